@@ -1,0 +1,266 @@
+"""Independent numpy / pure-Python restatement of the reference chain.
+
+Second, independent reading of the C# (written separately from
+oracle/qpsk_oracle.c) used only to cross-check the C oracle on small inputs.
+Float ops use numpy float32 scalars/arrays (IEEE single, one rounding per op),
+double ops use Python floats; no op is fused.
+
+References: FIRFilter.cs:144-211, MuellerMuller.cs:52-190,
+CostasLoopQpsk.cs:29-92, QPSKDeModulator.cs:39-56,304-408, RRC-filter.cs:16-75.
+"""
+from __future__ import annotations
+
+import math
+from fractions import Fraction
+
+import numpy as np
+
+F = np.float32
+
+
+def rrc_taps(span, beta, fs, rs):
+    """RRC-filter.cs:16-75 (double)."""
+    sps = int(round(fs / rs))  # Python round() is half-even like Math.Round
+    span_i = int(round(span))
+    taps = span_i * sps + 1
+    mid = (taps - 1) // 2
+    h = []
+    for n in range(taps):
+        t = (n - mid) / float(sps)
+        if abs(t) < 1e-8:
+            v = 1.0 + beta * (4.0 / math.pi - 1.0)
+        elif abs(abs(t) - 1.0 / (4.0 * beta)) < 1e-8:
+            v = (beta / math.sqrt(2.0)) * ((1.0 + 2.0 / math.pi) * math.sin(math.pi / (4.0 * beta))
+                                           + (1.0 - 2.0 / math.pi) * math.cos(math.pi / (4.0 * beta)))
+        else:
+            num = math.sin(math.pi * t * (1.0 - beta)) + 4.0 * beta * t * math.cos(math.pi * t * (1.0 + beta))
+            den = math.pi * t * (1.0 - math.pow(4.0 * beta * t, 2.0))
+            v = num / den
+        h.append(v)
+    e = 0.0
+    for v in h:
+        e += v * v
+    nrm = math.sqrt(e)
+    return np.array([v / nrm for v in h], dtype=np.float64)
+
+
+def fir_real_taps(h_f32, x_iq, lanes=8):
+    """ComplexFIRFilter.Filter over a whole buffer with imag taps = 0,
+    vectorised over output index; per-output summation order of the C#
+    Vector<float> path (FIRFilter.cs:156-192)."""
+    h = np.asarray(h_f32, dtype=F)
+    T = h.size
+    x = np.asarray(x_iq, dtype=F).reshape(-1, 2)
+    n = x.shape[0]
+    xp = np.concatenate([np.zeros((T - 1, 2), F), x])
+    hrev = h[::-1].copy()
+    zero = F(0)
+    out = np.zeros((n, 2), F)
+    for comp in range(2):
+        other = 1 - comp
+        win = lambda k, c: xp[k:k + n, c]
+        def term(k):
+            # (hi*xi) - (hq*xq) for I ; (hi*xq) + (hq*xi) for Q, hq = 0
+            if comp == 0:
+                return (hrev[k] * win(k, 0)) - (zero * win(k, 1))
+            return (hrev[k] * win(k, 1)) + (zero * win(k, 0))
+        acc = np.zeros(n, F)
+        if lanes > 1:
+            nvec = T - T % lanes
+            for l in range(lanes):
+                a = np.zeros(n, F)
+                for i in range(0, nvec, lanes):
+                    a = a + term(i + l)
+                acc = acc + a
+            for k in range(nvec, T):
+                acc = acc + term(k)
+        else:
+            for k in range(T):
+                acc = acc + term(k)
+        out[:, comp] = acc
+    return out.reshape(-1)
+
+
+def mm_gains(bn):
+    zeta = 1.0 / math.sqrt(2.0)
+    wn = ((2.0 * math.pi * bn) / (zeta + 0.25) / zeta)
+    den = 1.0 + 2.0 * zeta * wn + wn * wn
+    return (4.0 * zeta * wn) / den, (4.0 * wn * wn) / den
+
+
+class MM:
+    """MuellerMuller.cs (single-call semantics incl. buffer carry)."""
+
+    def __init__(self, sps, kp, ki):
+        self.sps, self.kp, self.ki = sps, kp, ki
+        self.base, self.mu, self.integ = 1, 0.0, 0.0
+        self.ps = (F(0), F(0))
+        self.pd = (F(0), F(0))
+        self.has_prev = False
+        self.buf = np.zeros((0, 2), F)
+
+    def process(self, x_iq, out_floats=None):
+        x = np.asarray(x_iq, dtype=F).reshape(-1, 2)
+        cap = x.size if out_floats is None else out_floats
+        self.buf = np.concatenate([self.buf, x])
+        cnt = self.buf.shape[0]
+        out = []
+        while self.base + 2 < cnt:
+            b = self.buf[self.base - 1:self.base + 3]
+            t = F(self.mu)
+            tm1, tm2, tp1 = t - F(1), t - F(2), t + F(1)
+            cm1 = -(t * tm1 * tm2) * (F(1) / F(6))
+            c0 = (tp1 * tm1 * tm2) * (F(1) / F(2))
+            c1 = -(tp1 * t * tm2) * (F(1) / F(2))
+            c2 = (tp1 * t * tm1) * (F(1) / F(6))
+            ci = cm1 * b[0, 0] + c0 * b[1, 0] + c1 * b[2, 0] + c2 * b[3, 0]
+            cq = cm1 * b[0, 1] + c0 * b[1, 1] + c1 * b[2, 1] + c2 * b[3, 1]
+            di = F(1) if ci >= 0 else F(-1)
+            dq = F(1) if cq >= 0 else F(-1)
+            if self.has_prev:
+                t1 = float(self.pd[0]) * float(ci) + float(self.pd[1]) * float(cq)
+                t2 = float(di) * float(self.ps[0]) + float(dq) * float(self.ps[1])
+                e = t1 - t2
+                self.integ += self.ki * e
+                corr = self.kp * e + self.integ
+                corr = min(corr, 0.1) if corr > 0.1 else corr
+                corr = -0.1 if corr < -0.1 else corr
+                adv = self.sps + corr
+            else:
+                self.has_prev = True
+                adv = self.sps
+            if 2 * len(out) + 1 >= cap:
+                break
+            out.append((ci, cq))
+            self.ps, self.pd = (ci, cq), (di, dq)
+            nt = (float(self.base) + self.mu) + adv
+            self.base = int(math.floor(nt))
+            self.mu = nt - float(self.base)
+            if self.base + 1 >= cnt:
+                break
+        consumed = min(max(0, self.base - 1), max(0, cnt - 3))
+        if consumed > 0:
+            self.buf = self.buf[consumed:]
+            self.base -= consumed
+        return np.array(out, dtype=F).reshape(-1)
+
+
+# ---- portable sincos (exact-fma emulation of or_sincos.h / qpsk_sincos.h) ----
+def _fma(a, b, c):
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
+_S = [-1.66666666666666324348e-01, 8.33333333332248946124e-03, -1.98412698298579493134e-04,
+      2.75573137070700676789e-06, -2.50507602534068634195e-08, 1.58969099521155010221e-10]
+_C = [4.16666666666666019037e-02, -1.38888888888741095749e-03, 2.48015872894767294178e-05,
+      -2.75573143513906633035e-07, 2.08757232129817482790e-09, -1.13596475577881948265e-11]
+
+
+def portable_sincos(x):
+    if not (abs(x) <= 1.0e300):
+        return math.nan, math.nan
+    if abs(x) > 1.0e6:
+        x = math.fmod(x, 6.28318530717958647693)
+    k = float(round(x * 6.36619772367581382433e-01))  # rint: half-even
+    r = _fma(-k, 1.57079632679489655800e+00, x)
+    r = _fma(-k, 6.12323399573676603587e-17, r)
+    r = _fma(-k, -1.49738490485916983e-33, r)
+    z = r * r
+    ps = _fma(z, _S[5], _S[4])
+    for c in (_S[3], _S[2], _S[1], _S[0]):
+        ps = _fma(z, ps, c)
+    v = z * r
+    ks = _fma(v, ps, r)
+    pc = _fma(z, _C[5], _C[4])
+    for c in (_C[3], _C[2], _C[1], _C[0]):
+        pc = _fma(z, pc, c)
+    hz = 0.5 * z
+    w = 1.0 - hz
+    kc = w + (((1.0 - w) - hz) + (z * z) * pc)
+    q = int(k) & 3
+    return [(ks, kc), (kc, -ks), (-ks, -kc), (-kc, ks)][q]
+
+
+class Costas:
+    """CostasLoopQpsk.cs:29-92."""
+
+    def __init__(self, fs, bw_hz, damping=0.707, portable=True):
+        bw = 2.0 * math.pi * bw_hz / fs
+        d = 1.0 + 2.0 * damping * bw + bw * bw
+        self.alpha = (4.0 * damping * bw) / d
+        self.beta = (4.0 * bw * bw) / d
+        self.theta = 0.0
+        self.freq = 0.0
+        self.portable = portable
+
+    def process(self, i, q):
+        if self.portable:
+            s, c = portable_sincos(self.theta)
+        else:
+            c, s = math.cos(self.theta), math.sin(self.theta)
+        mi = float(i) * c + float(q) * s
+        mq = float(q) * c - float(i) * s
+        oi, oq = F(mi), F(mq)
+        ei = 1.0 if oi >= 0 else -1.0
+        eq = 1.0 if oq >= 0 else -1.0
+        pe = ei * mq - eq * mi
+        self.freq += self.beta * pe
+        self.theta += self.freq + self.alpha * pe
+        if self.theta > math.pi:
+            self.theta -= 2.0 * math.pi
+        elif self.theta < -math.pi:
+            self.theta += 2.0 * math.pi
+        return oi, oq
+
+
+def decode_bits(rot, differential=True, state=None):
+    """QPSKDeModulator.cs:372-408 + AppendDeltaBits/AppendDecisionBits."""
+    st = state if state is not None else {"have": False, "p": (F(0), F(0))}
+    out = []
+    for ri, rq in rot:
+        di = F(1) if ri >= 0 else F(-1)
+        dq = F(1) if rq >= 0 else F(-1)
+        if differential:
+            if not st["have"]:
+                st["p"] = (di, dq)
+                st["have"] = True
+                continue
+            pi_, pq = st["p"]
+            dli = di * pi_ + dq * pq
+            dlq = dq * pi_ - di * pq
+            st["p"] = (di, dq)
+            if abs(dli) >= abs(dlq):
+                out.append("00" if dli >= 0 else "11")
+            else:
+                out.append("01" if dlq >= 0 else "10")
+        else:
+            if di < 0:
+                out.append("00" if dq < 0 else "01")
+            else:
+                out.append("11" if dq >= 0 else "10")
+    return "".join(out), st
+
+
+class RefDemod:
+    """QPSKDeModulator.DeModulate (FLL off), independent model."""
+
+    def __init__(self, fs, rs, alpha, span, ssbw=1e-4, clbw=120.0, differential=True, lanes=8,
+                 portable=True):
+        self.h = rrc_taps(float(span), float(F(alpha)), fs, rs).astype(F)
+        kp, ki = mm_gains(ssbw)
+        self.mm = MM(fs / float(rs), kp, ki)
+        self.costas = Costas(float(rs), rs / clbw, 0.707, portable)
+        self.lanes = lanes
+        self.hist = np.zeros(2 * (self.h.size - 1), F)
+        self.diff = {"have": False, "p": (F(0), F(0))}
+        self.differential = differential
+
+    def demodulate(self, iq):
+        iq = np.asarray(iq, dtype=F)
+        xx = np.concatenate([self.hist, iq])
+        y = fir_real_taps(self.h, xx, self.lanes)[self.hist.size:]
+        self.hist = xx[-self.hist.size:] if self.hist.size else self.hist
+        syms = self.mm.process(y, iq.size).reshape(-1, 2)
+        rot = [self.costas.process(s[0], s[1]) for s in syms]
+        bits, self.diff = decode_bits(rot, self.differential, self.diff)
+        return bits, np.array(rot, dtype=F).reshape(-1), y
