@@ -1,0 +1,186 @@
+/*
+ * qpsk_demod.h -- C ABI of the MI355X-native batched QPSK demodulation chain.
+ *
+ * This is the drop-in boundary for the reference's QPSKDeModulator C# class
+ * (NustyFrozen/QPSK-Modulator-Demodulator, Modulation-Simulation/QPSKDeModulator.cs).
+ * The reference has no FFI layer; its boundary *is* that public class.  A C#
+ * host binds these entry points with [DllImport("qpsk_demod")] (see
+ * INTEGRATION.md); one handle serves a batch of S independent streams, each of
+ * which behaves exactly like one QPSKDeModulator instance.
+ *
+ * Conventions (QPSKDeModulator.cs:339-425):
+ *  - input is interleaved float32 I,Q; every call continues the previous call's
+ *    FIR / FLL / Mueller-Muller / Costas / differential-decode state;
+ *  - an odd float count is QPSK_ERR_ARGUMENT (ArgumentException, :347-348);
+ *  - a zero-length call returns no bits and leaves the state untouched (:350-351);
+ *  - the caller owns every I/O buffer, the library owns device buffers and the
+ *    per-stream state; a handle is not thread-safe (one caller thread per
+ *    handle), distinct handles are independent.
+ * Every function returns an int status: 0 = ok, < 0 = error, message in
+ * qpsk_last_error().
+ */
+#ifndef QPSK_DEMOD_H
+#define QPSK_DEMOD_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QPSK_ABI_VERSION 1
+
+/* status codes -> the C# exception each one replaces */
+#define QPSK_OK 0
+#define QPSK_ERR_ARGUMENT (-1)        /* ArgumentException (odd length, empty marker) */
+#define QPSK_ERR_ARGUMENT_NULL (-2)   /* ArgumentNullException (QPSKDeModulator.cs:341,429) */
+#define QPSK_ERR_OUT_OF_RANGE (-3)    /* ArgumentOutOfRangeException (Band-Edge Filter.cs:42-45) */
+#define QPSK_ERR_DEVICE (-4)          /* HIP runtime failure */
+#define QPSK_ERR_CAPACITY (-5)        /* call larger than the handle's max_samples_per_call */
+#define QPSK_ERR_STATE (-6)           /* symbol-sync carry buffer overflow */
+
+/* where a pointer lives */
+#define QPSK_MEM_HOST 0
+#define QPSK_MEM_DEVICE 1
+
+/* what one call produces */
+#define QPSK_MODE_DEMODULATE 0        /* DeModulate: bits (+ optional symbols) */
+#define QPSK_MODE_CONSTELLATION 1     /* deModulateConstellation: symbols only, diff state untouched */
+
+/* Mirrors the QPSKDeModulator primary constructor 1:1 (QPSKDeModulator.cs:11-18)
+ * plus the batch / device knobs. */
+typedef struct qpsk_demod_params {
+    int32_t sample_rate;            /* int SampleRate                                   */
+    int32_t symbol_rate;            /* int SymbolRate                                   */
+    float rrc_alpha;                /* float RrcAlpha = 0.9f                            */
+    int32_t rrc_span;               /* int rrcSpan = 6                                  */
+    double symbol_sync_bandwidth;   /* double SymbolSyncBandwith = 0.0001               */
+    double costas_loop_bandwidth;   /* double CostasLoopBandwith = 120                  */
+    double cfo_loop_bandwidth;      /* double CFOLoopBandwith = 0.0001f                 */
+    int32_t differential;           /* bool differentialEncoding = true                 */
+    int32_t enable_fll;             /* 0 = reference DeModulate (fll.Process disabled, :359) */
+    int32_t vector_lanes;           /* Vector<float>.Count whose summation order the FIR
+                                       reproduces: 8 (x64 AVX2, default), 4 (ARM64), 1 (no SIMD) */
+    int32_t device;                 /* HIP device ordinal                               */
+    int64_t max_samples_per_call;   /* complex samples per stream per call (device buffers) */
+    int32_t reserved[8];
+} qpsk_demod_params;
+
+typedef struct qpsk_demod qpsk_demod;
+
+/* Fill defaults exactly as the C# optional parameters. */
+void qpsk_demod_params_init(qpsk_demod_params *p, int32_t sample_rate, int32_t symbol_rate);
+
+/* new QPSKDeModulator(...) x n_streams  (QPSKDeModulator.cs:11-56) */
+int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod **out);
+int qpsk_demod_destroy(qpsk_demod *h);
+
+/* Bind the handle to a caller-owned hipStream_t (NULL = library-owned stream). */
+int qpsk_demod_set_stream(qpsk_demod *h, void *hip_stream);
+
+/*
+ * One DeModulate (mode 0) or deModulateConstellation (mode 1) call on every
+ * stream of the batch  (QPSKDeModulator.cs:345-425 / :427-455).
+ *
+ * iq        [n_streams][stride_floats] float32, stream s holds
+ *           2*len(s) floats, len(s) = lengths ? lengths[s] : n_samples
+ * bits      [n_streams][bits_stride_bytes] raw demodulated bits of this call,
+ *           packed MSB-first (BitPacker order, HelperFunctions.cs:14-29), before
+ *           any TSC strip; may be NULL in mode 1
+ * n_bits    [n_streams] bit counts (2 per symbol; the very first symbol of a
+ *           differential stream yields none, :390-395)
+ * syms      [n_streams][syms_stride_floats] rotated Costas output symbols
+ *           (interleaved I,Q) or NULL
+ * n_syms    [n_streams] symbol counts or NULL
+ * mem       QPSK_MEM_HOST or QPSK_MEM_DEVICE for every pointer above
+ * The call is synchronous for host pointers and stream-ordered for device ones.
+ */
+int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t stride_floats,
+                       int64_t n_samples, const int64_t *lengths, int32_t mem, uint8_t *bits,
+                       int64_t bits_stride_bytes, int64_t *n_bits, float *syms,
+                       int64_t syms_stride_floats, int64_t *n_syms);
+
+/* Upper bounds a caller sizes outputs with, for a call of n_samples per stream. */
+int64_t qpsk_demod_max_symbols(const qpsk_demod *h, int64_t n_samples);
+
+/* First ordinal occurrence of tsc (a '0'/'1' string) in a packed bit row, i.e.
+ * rx.IndexOf(_tsc, StringComparison.Ordinal) (QPSKDeModulator.cs:413-422).
+ * Returns the bit index just past the TSC, or -1. */
+int64_t qpsk_tsc_find(const uint8_t *bits, int64_t n_bits, const char *tsc);
+
+/* Per-stage device times (ms) of the last process() call, measured with HIP
+ * events on the handle's stream when timing is enabled.
+ * ms[0] = FLL, ms[1] = matched-filter FIR, ms[2] = symbol-sync + Costas + decode,
+ * ms[3] = whole call.  Returns the number of entries written. */
+int qpsk_demod_enable_timing(qpsk_demod *h, int32_t on);
+int qpsk_demod_stage_times(const qpsk_demod *h, float *ms, int32_t n);
+
+/* Design products, for parity checks against the reference constructor. */
+int qpsk_demod_rrc_taps(const qpsk_demod *h, float *taps, int32_t cap);
+int qpsk_demod_gains(const qpsk_demod *h, double *mm_sps, double *kp, double *ki,
+                     double *costas_alpha, double *costas_beta);
+int qpsk_demod_fll_taps(const qpsk_demod *h, float *lower_iq, float *upper_iq, int32_t cap_floats);
+
+/* Constructor math without a device: RRC taps (float, as widened by
+ * ToInterleavedIQRealTaps, QPSKDeModulator.cs:278-288), gains[5] = {M&M sps,
+ * kp, ki, Costas alpha, Costas beta}, FLL band-edge taps (interleaved, 80
+ * floats each).  Returns the tap count or an error (same validation as create). */
+int qpsk_demod_design(const qpsk_demod_params *p, float *rrc_taps, int32_t cap, double *gains,
+                      float *fll_lower_iq, float *fll_upper_iq);
+
+/* Loop state snapshot, one record per stream (checkpoint / chunk carry). */
+int64_t qpsk_demod_state_bytes(const qpsk_demod *h);
+int qpsk_demod_get_state(const qpsk_demod *h, void *host_buf);
+int qpsk_demod_set_state(qpsk_demod *h, const void *host_buf);
+
+/* ---------------------------------------------------------------------------
+ * Byte framer (DeModulateBytes, QPSKDeModulator.cs:169-259), batched: one
+ * framer per stream fed with the packed bits of each process() call.
+ */
+typedef struct qpsk_framer qpsk_framer;
+int qpsk_framer_create(int32_t n_streams, const uint8_t *start_marker, int32_t n_start,
+                       const uint8_t *end_marker, int32_t n_end, int64_t ring_capacity,
+                       qpsk_framer **out);
+int qpsk_framer_destroy(qpsk_framer *f);
+/* DeModulateBytes takes its markers per call; change them without touching
+ * the framer state. */
+int qpsk_framer_set_markers(qpsk_framer *f, const uint8_t *start_marker, int32_t n_start,
+                            const uint8_t *end_marker, int32_t n_end);
+/* Feed one call's (post-TSC) bits for every stream (host memory); payload[s]
+ * receives the completed frame of this call if any (length in n_payload[s],
+ * 0 = none), exactly like one DeModulateBytes return value. */
+int qpsk_framer_push(qpsk_framer *f, const uint8_t *bits, int64_t bits_stride_bytes,
+                     const int64_t *bit_offset, const int64_t *n_bits, uint8_t *payload,
+                     int64_t payload_stride, int64_t *n_payload);
+
+/* ---------------------------------------------------------------------------
+ * Synthetic batched input (QPSKModulator.Modulate + the test bench channel),
+ * generated in device memory.  Stream s draws its payload from
+ * splitmix64(seed ^ s); tx_bits receives the payload bits (packed MSB-first).
+ * cfo_hz: per-stream carrier offset drawn U[-cfo_hz, +cfo_hz] (0 = clean
+ * ±ppm LO pair), multipath: 4-tap channel [1, .25e^{j.7}, .1e^{-j1.9}, .05],
+ * esn0_db: AWGN Es/N0 (>= 200 = none).
+ */
+typedef struct qpsk_synth_params {
+    int32_t sample_rate, symbol_rate;
+    double rrc_alpha;
+    int32_t rrc_span;
+    int32_t differential;
+    uint64_t seed;
+    double lo_ppm;
+    double cfo_hz;
+    int32_t multipath;
+    double esn0_db;
+    int32_t reserved[8];
+} qpsk_synth_params;
+void qpsk_synth_params_init(qpsk_synth_params *p, int32_t sample_rate, int32_t symbol_rate);
+int qpsk_synth_generate(const qpsk_synth_params *p, int32_t device, void *hip_stream,
+                        int32_t n_streams, int64_t n_samples, float *iq_dev,
+                        int64_t stride_floats, uint8_t *tx_bits_dev, int64_t bits_stride_bytes);
+
+const char *qpsk_last_error(void);
+int qpsk_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -118,6 +118,7 @@ def lib():
         L.or_nco_free.argtypes = [C.c_void_p]
         L.or_nco_next.argtypes = [C.c_void_p, _f64p, _f64p]
         L.or_apply_lo_pair.argtypes = [C.c_void_p, C.c_void_p, _f32p, C.c_long]
+        L.or_sincos_batch.argtypes = [_f64p, C.c_long, _f64p, _f64p]
         _lib = L
     return _lib
 
@@ -400,3 +401,13 @@ def apply_lo_pair(tx: OracleNCO, rx: OracleNCO, iq):
     iq = _f32(iq).copy()
     lib().or_apply_lo_pair(tx._h, rx._h, _fp(iq), iq.size // 2)
     return iq
+
+
+def sincos(x):
+    """Portable sincos of the oracle (or_sincos.h) over a float64 array."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    s = np.zeros_like(x)
+    c = np.zeros_like(x)
+    lib().or_sincos_batch(x.ctypes.data_as(_f64p), x.size, s.ctypes.data_as(_f64p),
+                          c.ctypes.data_as(_f64p))
+    return s, c

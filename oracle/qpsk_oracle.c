@@ -1141,3 +1141,9 @@ void or_apply_lo_pair(or_nco *tx, or_nco *rx, float *iq, long n_complex)
         iq[2 * i + 1] = (float)yi;
     }
 }
+
+/* Portable sincos (or_sincos.h) over an array, for the test sweeps. */
+void or_sincos_batch(const double *x, long n, double *s, double *c)
+{
+    for (long i = 0; i < n; i++) or_sincos(x[i], &s[i], &c[i]);
+}

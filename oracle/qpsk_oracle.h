@@ -114,6 +114,7 @@ void or_nco_next(or_nco *n, double *re, double *im);
 /* testAtDataLevel.cs:39-42: iq[i] *= tx.Next() * conj(rx.Next()) in double, cast to float */
 void or_apply_lo_pair(or_nco *tx, or_nco *rx, float *iq, long n_complex);
 uint64_t or_splitmix64(uint64_t *state);
+void or_sincos_batch(const double *x, long n, double *s, double *c);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,68 @@
+// qpsk_kernels.h -- launch interface of the HIP kernels (qpsk_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "qpsk_state.h"
+
+namespace qpsk {
+
+constexpr int kModeDemodulate = 0;
+constexpr int kModeConstellation = 1;
+
+// Reversed RRC taps (ComplexFIRFilter._tapsIRev), passed by value -> SGPRs.
+struct TapsRev {
+    float h[kMaxTapsSpecialised];
+};
+
+struct FirArgs {
+    const float *x;        // [S][x_stride] float2 input
+    int64_t x_stride;      // in float2
+    const float *hist;     // [S][T-1] float2: previous call's last T-1 inputs
+    const int64_t *lengths;
+    int64_t n;             // uniform length when lengths == nullptr
+    float *y;              // [S][y_stride] float2 output at y_offset
+    int64_t y_stride;
+    int64_t y_offset;
+};
+
+struct LoopArgs {
+    float *mf;             // [S][mf_stride] float2, MF output at kMfPrefix
+    int64_t mf_stride;
+    float *carry;          // [S][kCarryMax] float2
+    const int64_t *lengths;
+    int64_t n;
+    StreamState *state;
+    uint32_t *bits;        // [S][bits_stride_words]
+    int64_t bits_stride_words;
+    int64_t bits_cap_words;
+    int64_t *n_bits;
+    float *syms;           // [S][syms_stride] float2 or nullptr
+    int64_t syms_stride;
+    int64_t syms_cap;
+    int64_t *n_syms;
+    int S;
+};
+
+struct FllArgs {
+    const float *x;
+    int64_t x_stride;
+    float *y;
+    int64_t y_stride;
+    float *delay;          // [S][2*kFllTaps] float2
+    const int64_t *lengths;
+    int64_t n;
+    StreamState *state;
+    int S;
+};
+
+// Returns true when a specialised tile kernel was used.
+bool launch_fir(const FirArgs &a, const TapsRev &taps, const float *hrev_dev, int T, int W, int S,
+                int64_t n_max, hipStream_t stream);
+void launch_fir_hist(const FirArgs &a, float *hist_new, int H, int S, hipStream_t stream);
+void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int lanes_per_block,
+                 hipStream_t stream);
+void launch_fll(const FllArgs &a, const FllParams &P, hipStream_t stream);
+
+}  // namespace qpsk

@@ -1,0 +1,522 @@
+// qpsk_kernels.hip -- hand-written CDNA4 (gfx950) kernels of the batched QPSK
+// demodulation chain.
+//
+//   fir_tile_kernel    RRC matched filter (ComplexFIRFilter.Filter, FIRFilter.cs:59-91,
+//                      144-211) for a [stream][time] batch; LDS-staged input tile
+//                      with (T-1)-sample halo, taps in SGPRs, the C# Vector<float>
+//                      lane summation order reproduced exactly.
+//   fir_generic_kernel same contract for tap counts / lane widths without a
+//                      specialised instantiation.
+//   fir_hist_kernel    carries the last T-1 input samples to the next call.
+//   loop_kernel        MuellerMuller.Process (MuellerMuller.cs:52-190) fused with
+//                      CostasLoopQpsk.Process (CostasLoopQpsk.cs:63-92), hard
+//                      decision, differential decode and MSB-first bit packing
+//                      (QPSKDeModulator.cs:372-408); one lane per stream.
+//   fll_kernel         FLLBandEdgeFilter.Process (Band-Edge Filter.cs:64-129),
+//                      one lane per stream.
+//
+// Compiled with -ffp-contract=off: every float/double op rounds exactly as the
+// reference C# (which never fuses a*b+c).  The only fma() calls are the explicit
+// ones inside the portable sincos (qpsk_sincos.h).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "qpsk_kernels.h"
+#include "qpsk_sincos.h"
+
+namespace qpsk {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// Matched-filter FIR
+// ---------------------------------------------------------------------------
+// LDS image of the input tile: one float2 per slot, 8 pad slots after every 64
+// samples so the stride-64 groups of a wave's reads fall on distinct banks.
+__device__ __forceinline__ int lds_slot(int i) { return i + ((i >> 6) << 3); }
+constexpr int lds_slots(int n) { return n + ((n >> 6) << 3) + 8; }
+
+constexpr int kFirThreads = 256;
+
+template <int T, int W, int Q, bool VEC>
+__global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRev taps) {
+    constexpr int TILE = kFirThreads * Q;
+    constexpr int NIN = TILE + T - 1;
+    constexpr int J = T / W;          // full Vector<float> blocks
+    constexpr int NVEC = J * W;
+    constexpr int TAIL = T - NVEC;    // scalar tail taps (FIRFilter.cs:183-192)
+    __shared__ f2 lds[lds_slots(NIN)];
+
+    const int s = blockIdx.y;
+    const int64_t tile0 = static_cast<int64_t>(blockIdx.x) * TILE;
+    const int64_t n = a.lengths ? a.lengths[s] : a.n;
+    if (tile0 >= n) return;
+    const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
+    const f2 *hist = reinterpret_cast<const f2 *>(a.hist) + static_cast<int64_t>(s) * (T - 1);
+    const int tid = threadIdx.x;
+
+    // Stage x[tile0-(T-1) .. tile0+TILE) ; t<0 from the previous call's history,
+    // t>=n as zeros (those outputs are not stored).
+    const int64_t g0 = tile0 - (T - 1);
+    if constexpr (VEC) {
+        // g0 is even (T odd) and rows are 16-B aligned: one float4 = 2 samples.
+        for (int p = tid; p < (NIN + 1) / 2; p += kFirThreads) {
+            const int64_t g = g0 + 2 * p;
+            f4 v;
+            if (g >= 0 && g + 1 < n) {
+                v = *reinterpret_cast<const f4 *>(x + g);
+            } else {
+                f2 lo = g < 0 ? hist[T - 1 + g] : (g < n ? x[g] : f2{0.f, 0.f});
+                f2 hi = (g + 1) < 0 ? hist[T + g] : ((g + 1) < n ? x[g + 1] : f2{0.f, 0.f});
+                v = f4{lo.x, lo.y, hi.x, hi.y};
+            }
+            *reinterpret_cast<f4 *>(&lds[lds_slot(2 * p)]) = v;
+        }
+    } else {
+        for (int i = tid; i < NIN; i += kFirThreads) {
+            const int64_t g = g0 + i;
+            lds[lds_slot(i)] = g < 0 ? hist[T - 1 + g] : (g < n ? x[g] : f2{0.f, 0.f});
+        }
+    }
+    __syncthreads();
+
+    // Thread -> outputs t0 + W*q, q < Q, t0 = 64*grp + r: a group of W threads
+    // covers one 64-sample LDS row of outputs.  The read of input t0 + c (c a
+    // compile-time offset) lands in slot 72*grp + r + c + 8*floor((r+c)/64);
+    // the floor is compile-time except when c mod 64 > 56, so almost every
+    // ds_read uses an immediate offset and the 8-slot row pad keeps the four
+    // groups of a half-wave on distinct banks.
+    static_assert(W * Q == 64, "specialised FIR expects W*Q == 64");
+    const int grp = tid / W, r = tid % W;
+    const f2 *row = lds + 72 * grp + r;
+    auto rd = [&](int c) -> f2 {
+        const int lo = c >> 6, hi = (c + W - 1) >> 6;
+        if (lo == hi) return row[c + 8 * lo];
+        return row[c + 8 * lo + ((r + (c & 63)) >= 64 ? 8 : 0)];
+    };
+    f2 acc[Q];
+    if constexpr (J == 0) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) acc[q] = f2{0.f, 0.f};
+    }
+#pragma unroll
+    for (int l = 0; l < W && J > 0; ++l) {
+        // Lane accumulator l of every output: sum_j hrev[jW+l] * x[t-T+1+jW+l],
+        // j ascending (FIRFilter.cs:165-174); u_i = x[t0 + l + W i] is shared by
+        // the Q outputs of this thread.
+        f2 A[Q];
+#pragma unroll
+        for (int i = 0; i < Q + J - 1; ++i) {
+            const f2 u = rd(l + W * i);
+            f2 p[Q];   // all products of u first, then the adds (no mul->add stall)
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int j = i - q;
+                if (j >= 0 && j < J) p[q] = taps.h[j * W + l] * u;
+            }
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int j = i - q;
+                if (j >= 0 && j < J) A[q] = (j == 0) ? p[q] : A[q] + p[q];
+            }
+        }
+        // Horizontal sum in lane order 0..W-1 (FIRFilter.cs:176-180).
+#pragma unroll
+        for (int q = 0; q < Q; ++q) acc[q] = (l == 0) ? A[q] : acc[q] + A[q];
+    }
+#pragma unroll
+    for (int k = 0; k < TAIL; ++k) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const f2 u = rd(W * q + NVEC + k);
+            acc[q] = acc[q] + taps.h[NVEC + k] * u;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < Q; ++q) lds[72 * grp + r + W * q] = acc[q];
+    __syncthreads();
+
+    f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride + a.y_offset;
+    if constexpr (VEC) {
+        for (int p = tid; p < TILE / 2; p += kFirThreads) {
+            const int64_t g = tile0 + 2 * p;
+            if (g + 1 < n) {
+                *reinterpret_cast<f4 *>(y + g) = *reinterpret_cast<const f4 *>(&lds[lds_slot(2 * p)]);
+            } else if (g < n) {
+                y[g] = lds[lds_slot(2 * p)];
+            }
+        }
+    } else {
+        for (int i = tid; i < TILE; i += kFirThreads) {
+            const int64_t g = tile0 + i;
+            if (g < n) y[g] = lds[lds_slot(i)];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void fir_generic_kernel(FirArgs a, const float *hrev, int T,
+                                                          int W) {
+    const int s = blockIdx.y;
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t n = a.lengths ? a.lengths[s] : a.n;
+    if (t >= n) return;
+    const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
+    const f2 *hist = reinterpret_cast<const f2 *>(a.hist) + static_cast<int64_t>(s) * (T - 1);
+    auto X = [&](int64_t g) -> f2 { return g < 0 ? hist[T - 1 + g] : x[g]; };
+    const int64_t w0 = t - T + 1;
+    f2 acc = f2{0.f, 0.f};
+    if (W > 1) {
+        const int nvec = T - T % W;
+        for (int l = 0; l < W; ++l) {
+            f2 A = f2{0.f, 0.f};
+            for (int i = 0; i < nvec; i += W) A = A + hrev[i + l] * X(w0 + i + l);
+            acc = acc + A;
+        }
+        for (int i = nvec; i < T; ++i) acc = acc + hrev[i] * X(w0 + i);
+    } else {
+        for (int i = 0; i < T; ++i) acc = acc + hrev[i] * X(w0 + i);
+    }
+    f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride + a.y_offset;
+    y[t] = acc;
+}
+
+// new_hist = last (T-1) samples of concat(old_hist, x[0..n))
+__global__ void fir_hist_kernel(FirArgs a, float *hist_new, int H, int S) {
+    const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (idx >= static_cast<int64_t>(S) * H) return;
+    const int s = static_cast<int>(idx / H);
+    const int k = static_cast<int>(idx % H);
+    const int64_t n = a.lengths ? a.lengths[s] : a.n;
+    const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
+    const f2 *ho = reinterpret_cast<const f2 *>(a.hist) + static_cast<int64_t>(s) * H;
+    f2 *hn = reinterpret_cast<f2 *>(hist_new) + static_cast<int64_t>(s) * H;
+    const int64_t m = n + k;
+    hn[k] = m < H ? ho[m] : x[m - H];
+}
+
+// ---------------------------------------------------------------------------
+// Symbol sync + carrier recovery + decode, one lane per stream
+// ---------------------------------------------------------------------------
+template <int MODE, bool DIFF, bool SYMS>
+__global__ __launch_bounds__(64) void loop_kernel(LoopArgs a, LoopParams P) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.S) return;
+    const int64_t n = a.lengths ? a.lengths[s] : a.n;
+    if (MODE == kModeDemodulate && n == 0) {   // QPSKDeModulator.cs:350-351
+        if (a.n_bits) a.n_bits[s] = 0;
+        if (a.n_syms) a.n_syms[s] = 0;
+        return;
+    }
+    StreamState st = a.state[s];
+    f2 *mf = reinterpret_cast<f2 *>(a.mf) + s * a.mf_stride;
+    const int R = st.carry_n;
+    f2 *buf = mf + kMfPrefix - R;             // logical queue index 0
+    const f2 *carry = reinterpret_cast<const f2 *>(a.carry) + static_cast<int64_t>(s) * kCarryMax;
+    for (int i = 0; i < R; ++i) buf[i] = carry[i];
+    const int64_t count = R + n;              // _bufCount after Append
+    const int64_t cap = n;                    // output span = 2n floats (QPSKDeModulator.cs:366)
+
+    int64_t base = st.base;
+    double mu = st.mu, integ = st.integ;
+    float psi = st.psi, psq = st.psq, pdi = st.pdi, pdq = st.pdq;
+    int has_prev = st.has_prev;
+    double theta = st.theta, freq = st.freq;
+    int diff_have = st.diff_have;
+    float dpi = st.diff_pi, dpq = st.diff_pq;
+    const double sps = P.sps, kp = P.kp, ki = P.ki, ca = P.c_alpha, cb = P.c_beta;
+    const double kTwoPi = 2.0 * 3.14159265358979311600;
+    const double kPi = 3.14159265358979311600;
+
+    uint32_t *bits = a.bits ? a.bits + s * a.bits_stride_words : nullptr;
+    f2 *syms = SYMS ? reinterpret_cast<f2 *>(a.syms) + s * a.syms_stride : nullptr;
+    const int64_t sym_cap = a.syms_cap;
+    uint32_t word = 0;
+    int wbits = 0;
+    int64_t widx = 0, nbits = 0, nsym = 0;
+    int err = st.error;
+
+    while (base + 2 < count) {
+        // CubicLagrange4 (MuellerMuller.cs:160-190), float
+        const f2 xm1 = buf[base - 1], x0 = buf[base], x1 = buf[base + 1], x2 = buf[base + 2];
+        const float t = static_cast<float>(mu);
+        const float tm1 = t - 1.0f, tm2 = t - 2.0f, tp1 = t + 1.0f;
+        const float cm1 = -(t * tm1 * tm2) * (1.0f / 6.0f);
+        const float c0 = (tp1 * tm1 * tm2) * (1.0f / 2.0f);
+        const float c1 = -(tp1 * t * tm2) * (1.0f / 2.0f);
+        const float c2 = (tp1 * t * tm1) * (1.0f / 6.0f);
+        const float ci = cm1 * xm1.x + c0 * x0.x + c1 * x1.x + c2 * x2.x;
+        const float cq = cm1 * xm1.y + c0 * x0.y + c1 * x1.y + c2 * x2.y;
+        const float di = ci >= 0.0f ? 1.0f : -1.0f;
+        const float dq = cq >= 0.0f ? 1.0f : -1.0f;
+        double adv;
+        if (has_prev) {   // M&M TED + PI filter (MuellerMuller.cs:78-91), double
+            const double t1 = static_cast<double>(pdi) * ci + static_cast<double>(pdq) * cq;
+            const double t2 = static_cast<double>(di) * psi + static_cast<double>(dq) * psq;
+            const double e = t1 - t2;
+            integ += ki * e;
+            double corr = kp * e + integ;
+            if (corr > 0.1) corr = 0.1;
+            if (corr < -0.1) corr = -0.1;
+            adv = sps + corr;
+        } else {
+            has_prev = 1;
+            adv = sps;
+        }
+        if (nsym >= cap) break;   // MuellerMuller.cs:101-102 (state kept, no emit)
+
+        // Costas (CostasLoopQpsk.cs:63-92): double NCO, float I/O
+        double sn, cs;
+        qpsk_sincos(theta, &sn, &cs);
+        const double mi = static_cast<double>(ci) * cs + static_cast<double>(cq) * sn;
+        const double mq = static_cast<double>(cq) * cs - static_cast<double>(ci) * sn;
+        const float ri = static_cast<float>(mi), rq = static_cast<float>(mq);
+        const float ei = ri >= 0.0f ? 1.0f : -1.0f;
+        const float eq = rq >= 0.0f ? 1.0f : -1.0f;
+        const double pe = static_cast<double>(ei) * mq - static_cast<double>(eq) * mi;
+        freq += cb * pe;
+        theta += freq + ca * pe;
+        if (theta > kPi) theta -= kTwoPi;
+        else if (theta < -kPi) theta += kTwoPi;
+        if (SYMS) {
+            if (nsym < sym_cap) syms[nsym] = f2{ri, rq};
+            else err |= 2;
+        }
+        if (MODE == kModeDemodulate) {
+            // Decision + differential decode (QPSKDeModulator.cs:379-407)
+            bool emit = true;
+            uint32_t b2 = 0;
+            if (DIFF) {
+                if (!diff_have) {
+                    dpi = ei; dpq = eq;
+                    diff_have = 1;
+                    emit = false;
+                } else {
+                    const float del_i = ei * dpi + eq * dpq;
+                    const float del_q = eq * dpi - ei * dpq;
+                    dpi = ei; dpq = eq;
+                    if (fabsf(del_i) >= fabsf(del_q)) b2 = del_i >= 0.0f ? 0u : 3u;  // 00 / 11
+                    else b2 = del_q >= 0.0f ? 1u : 2u;                               // 01 / 10
+                }
+            } else {
+                b2 = (ei < 0.0f ? 0u : 2u) | (eq < 0.0f ? 0u : 1u);                  // :304-318
+            }
+            if (emit) {
+                word = (word << 2) | b2;
+                wbits += 2;
+                nbits += 2;
+                if (wbits == 32) {
+                    if (widx < a.bits_cap_words) bits[widx] = __builtin_bswap32(word);
+                    else err |= 2;
+                    ++widx;
+                    word = 0;
+                    wbits = 0;
+                }
+            }
+        }
+        ++nsym;
+        psi = ci; psq = cq;
+        pdi = di; pdq = dq;
+        const double nt = static_cast<double>(base) + mu + adv;   // MuellerMuller.cs:113
+        const double fl = floor(nt);
+        base = static_cast<int64_t>(fl);
+        mu = nt - fl;
+        if (base + 1 >= count) break;
+    }
+    if (MODE == kModeDemodulate && wbits > 0) {
+        if (widx < a.bits_cap_words) bits[widx] = __builtin_bswap32(word << (32 - wbits));
+        else err |= 2;
+    }
+    // Drop consumed samples, keep the rest for the next call (MuellerMuller.cs:123-133)
+    int64_t consumed = base - 1 > 0 ? base - 1 : 0;
+    const int64_t keep_min = count - 3 > 0 ? count - 3 : 0;
+    if (keep_min < consumed) consumed = keep_min;
+    int64_t keep = count - consumed;
+    if (keep > kCarryMax) {
+        err |= 1;
+        consumed = count - kCarryMax;
+        keep = kCarryMax;
+    }
+    f2 *carry_w = reinterpret_cast<f2 *>(a.carry) + static_cast<int64_t>(s) * kCarryMax;
+    for (int64_t i = 0; i < keep; ++i) carry_w[i] = buf[consumed + i];
+    st.base = static_cast<int32_t>(base - consumed);
+    st.carry_n = static_cast<int32_t>(keep);
+    st.mu = mu; st.integ = integ;
+    st.psi = psi; st.psq = psq; st.pdi = pdi; st.pdq = pdq;
+    st.has_prev = has_prev;
+    st.theta = theta; st.freq = freq;
+    if (MODE == kModeDemodulate) {
+        st.diff_have = diff_have;
+        st.diff_pi = dpi;
+        st.diff_pq = dpq;
+    }
+    st.error = err;
+    a.state[s] = st;
+    if (a.n_bits) a.n_bits[s] = MODE == kModeDemodulate ? nbits : 0;
+    if (a.n_syms) a.n_syms[s] = nsym;
+}
+
+// ---------------------------------------------------------------------------
+// Band-Edge FLL, one lane per stream (exact reference order)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fll_dot(const float *taps_rev, const f2 *win, int W, float *oi,
+                                        float *oq) {
+    constexpr int N = kFllTaps;
+    float acc_i = 0.f, acc_q = 0.f;
+    if (W > 1) {
+        const int nvec = N - N % W;
+        for (int l = 0; l < W; ++l) {
+            float vi = 0.f, vq = 0.f;
+            for (int i = 0; i < nvec; i += W) {
+                const float hi = taps_rev[2 * (i + l)], hq = taps_rev[2 * (i + l) + 1];
+                const f2 x = win[i + l];
+                vi = vi + ((hi * x.x) - (hq * x.y));
+                vq = vq + ((hi * x.y) + (hq * x.x));
+            }
+            acc_i += vi;
+            acc_q += vq;
+        }
+        for (int i = nvec; i < N; ++i) {
+            const float hi = taps_rev[2 * i], hq = taps_rev[2 * i + 1];
+            const f2 x = win[i];
+            acc_i += (hi * x.x) - (hq * x.y);
+            acc_q += (hi * x.y) + (hq * x.x);
+        }
+    } else {
+        for (int i = 0; i < N; ++i) {
+            const float hi = taps_rev[2 * i], hq = taps_rev[2 * i + 1];
+            const f2 x = win[i];
+            acc_i += (hi * x.x) - (hq * x.y);
+            acc_q += (hi * x.y) + (hq * x.x);
+        }
+    }
+    *oi = acc_i;
+    *oq = acc_q;
+}
+
+__global__ __launch_bounds__(64) void fll_kernel(FllArgs a, FllParams P) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.S) return;
+    const int64_t n = a.lengths ? a.lengths[s] : a.n;
+    if (n == 0) return;
+    constexpr int N = kFllTaps;
+    StreamState st = a.state[s];
+    const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
+    f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride;
+    // 2N delay line (FIRFilter.cs:18-22), shared by both band-edge filters since
+    // both are fed the same mixed sample.
+    f2 *dl = reinterpret_cast<f2 *>(a.delay) + static_cast<int64_t>(s) * 2 * N;
+    float phase = st.fll_phase, freq = st.fll_freq;
+    int pos = st.fll_pos;
+    const float two_pi = 2.0f * 3.14159274101257324219f;
+    for (int64_t t = 0; t < n; ++t) {
+        const f2 in = x[t];
+        float sn, cs;
+        qpsk_sincosf(phase, &sn, &cs);
+        const float oi = in.x * cs - in.y * sn;
+        const float oq = in.x * sn + in.y * cs;
+        y[t] = f2{oi, oq};
+        dl[pos] = f2{oi, oq};
+        dl[pos + N] = f2{oi, oq};
+        int start = pos + 1;
+        if (start >= N) start -= N;
+        float upi, upq, loi, loq;
+        fll_dot(P.upper_rev, dl + start, P.lanes, &upi, &upq);   // filterUpper first (:115)
+        fll_dot(P.lower_rev, dl + start, P.lanes, &loi, &loq);
+        const float pu = upi * upi + upq * upq;
+        const float pl = loi * loi + loq * loq;
+        const float err = pl - pu;
+        freq += P.beta * err;
+        phase += freq + P.alpha * err;
+        if (phase > two_pi || phase < -two_pi) phase = remainderf(phase, two_pi);
+        if (freq > P.max_freq) freq = P.max_freq;
+        else if (freq < P.min_freq) freq = P.min_freq;
+        ++pos;
+        if (pos == N) pos = 0;
+    }
+    st.fll_phase = phase;
+    st.fll_freq = freq;
+    st.fll_pos = pos;
+    a.state[s] = st;
+}
+
+// ---------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------
+template <int T>
+static bool launch_fir_w8(const FirArgs &a, const TapsRev &taps, int S, int64_t n_max, bool vec,
+                          hipStream_t stream) {
+    constexpr int Q = 8;
+    const int64_t tiles = (n_max + kFirThreads * Q - 1) / (kFirThreads * Q);
+    dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(S));
+    if (vec)
+        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, true>), grid, dim3(kFirThreads), 0, stream, a, taps);
+    else
+        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, false>), grid, dim3(kFirThreads), 0, stream, a, taps);
+    return true;
+}
+
+bool launch_fir(const FirArgs &a, const TapsRev &taps, const float *hrev_dev, int T, int W, int S,
+                int64_t n_max, hipStream_t stream) {
+    if (n_max <= 0 || S <= 0) return true;
+    const bool vec = (T % 2 == 1) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) &&
+                     (a.x_stride % 2 == 0) && ((reinterpret_cast<uintptr_t>(a.y) & 15) == 0) &&
+                     (a.y_stride % 2 == 0) && (a.y_offset % 2 == 0);
+    if (W == 8) {
+        switch (T) {
+        case 13: return launch_fir_w8<13>(a, taps, S, n_max, vec, stream);
+        case 17: return launch_fir_w8<17>(a, taps, S, n_max, vec, stream);
+        case 21: return launch_fir_w8<21>(a, taps, S, n_max, vec, stream);
+        case 33: return launch_fir_w8<33>(a, taps, S, n_max, vec, stream);
+        case 41: return launch_fir_w8<41>(a, taps, S, n_max, vec, stream);
+        case 49: return launch_fir_w8<49>(a, taps, S, n_max, vec, stream);
+        case 65: return launch_fir_w8<65>(a, taps, S, n_max, vec, stream);
+        case 97: return launch_fir_w8<97>(a, taps, S, n_max, vec, stream);
+        case 129: return launch_fir_w8<129>(a, taps, S, n_max, vec, stream);
+        default: break;
+        }
+    }
+    const int threads = 256;
+    dim3 grid(static_cast<unsigned>((n_max + threads - 1) / threads), static_cast<unsigned>(S));
+    hipLaunchKernelGGL(fir_generic_kernel, grid, dim3(threads), 0, stream, a, hrev_dev, T, W);
+    return false;
+}
+
+void launch_fir_hist(const FirArgs &a, float *hist_new, int H, int S, hipStream_t stream) {
+    if (H <= 0 || S <= 0) return;
+    const int64_t total = static_cast<int64_t>(S) * H;
+    const int threads = 256;
+    hipLaunchKernelGGL(fir_hist_kernel, dim3(static_cast<unsigned>((total + threads - 1) / threads)),
+                       dim3(threads), 0, stream, a, hist_new, H, S);
+}
+
+void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int lanes_per_block,
+                 hipStream_t stream) {
+    const int threads = lanes_per_block > 0 ? lanes_per_block : 64;
+    dim3 grid((a.S + threads - 1) / threads);
+    const bool syms = a.syms != nullptr;
+    const bool diff = P.differential != 0;
+    if (mode == kModeConstellation) {
+        hipLaunchKernelGGL((loop_kernel<kModeConstellation, false, true>), grid, dim3(threads), 0,
+                           stream, a, P);
+    } else if (diff) {
+        if (syms)
+            hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, true>), grid, dim3(threads), 0, stream, a, P);
+        else
+            hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, false>), grid, dim3(threads), 0, stream, a, P);
+    } else {
+        if (syms)
+            hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, true>), grid, dim3(threads), 0, stream, a, P);
+        else
+            hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, false>), grid, dim3(threads), 0, stream, a, P);
+    }
+}
+
+void launch_fll(const FllArgs &a, const FllParams &P, hipStream_t stream) {
+    const int threads = 64;
+    hipLaunchKernelGGL(fll_kernel, dim3((a.S + threads - 1) / threads), dim3(threads), 0, stream, a, P);
+}
+
+}  // namespace qpsk

@@ -1,0 +1,487 @@
+// qpsk_runtime.hip -- host runtime behind the C ABI (include/qpsk_demod.h):
+// handle = a batch of S reference QPSKDeModulator instances living on one
+// MI355X.  Owns the device buffers and the per-stream state, orders the kernels
+// of one DeModulate call on one HIP stream:
+//
+//     [FLL] -> matched-filter FIR -> FIR history carry -> M&M+Costas+decode
+//
+// Device layout (HBM, stream-major so every stage reads/writes each stream's
+// time axis contiguously):
+//   in      [S][n_max]              float2  staging for host input
+//   fll_out [S][n_max]              float2  (FLL mode)
+//   hist    2 x [S][T-1]            float2  FIR delay line (ping-pong)
+//   mf      [S][64 + n_max]         float2  matched-filter output; the 64-slot
+//                                           prefix receives the M&M carry
+//   carry   [S][64]                 float2  M&M retained samples
+//   state   [S]                     StreamState
+//   bits    [S][words]              uint32  MSB-first packed bits
+//   syms    [S][syms_cap]           float2  rotated symbols (on request)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "qpsk_demod.h"
+#include "qpsk_design.h"
+#include "qpsk_kernels.h"
+
+using namespace qpsk;
+
+namespace {
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return fail(QPSK_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <typename T>
+int dev_alloc(T **p, size_t count) {
+    *p = nullptr;
+    if (count == 0) return QPSK_OK;
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(p), count * sizeof(T));
+    if (e != hipSuccess)
+        return fail(QPSK_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return QPSK_OK;
+}
+}  // namespace
+
+struct qpsk_demod {
+    qpsk_demod_params p{};
+    int S = 0;
+    int T = 0;
+    int W = 8;
+    LoopDesign d;
+    TapsRev taps{};
+    LoopParams lp{};
+    FllParams fp{};
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int64_t n_max = 0;
+    int64_t mf_stride = 0;       // float2
+    int64_t bits_words = 0;      // per stream
+    int64_t syms_cap = 0;        // per stream
+    float *d_hrev = nullptr;
+    float *d_in = nullptr;
+    float *d_fll_out = nullptr;
+    float *d_hist[2] = {nullptr, nullptr};
+    int hist_cur = 0;
+    float *d_mf = nullptr;
+    float *d_carry = nullptr;
+    StreamState *d_state = nullptr;
+    float *d_fll_delay = nullptr;
+    uint32_t *d_bits = nullptr;
+    float *d_syms = nullptr;
+    int64_t *d_counts = nullptr;     // [2][S]: n_bits, n_syms
+    int64_t *d_lengths = nullptr;
+    int64_t *h_counts = nullptr;     // pinned
+    bool timing = false;
+    hipEvent_t ev[4] = {};
+    float stage_ms[4] = {0, 0, 0, 0};
+};
+
+extern "C" {
+
+int qpsk_abi_version(void) { return QPSK_ABI_VERSION; }
+
+const char *qpsk_last_error(void) { return g_last_error.c_str(); }
+
+void qpsk_demod_params_init(qpsk_demod_params *p, int32_t sample_rate, int32_t symbol_rate) {
+    std::memset(p, 0, sizeof(*p));
+    p->sample_rate = sample_rate;
+    p->symbol_rate = symbol_rate;
+    p->rrc_alpha = 0.9f;                       // QPSKDeModulator.cs:14-18 defaults
+    p->rrc_span = 6;
+    p->symbol_sync_bandwidth = 0.0001;
+    p->costas_loop_bandwidth = 120;
+    p->cfo_loop_bandwidth = static_cast<double>(0.0001f);
+    p->differential = 1;
+    p->enable_fll = 0;
+    p->vector_lanes = 8;
+    p->device = 0;
+    p->max_samples_per_call = 1 << 20;
+}
+
+int64_t qpsk_demod_max_symbols(const qpsk_demod *h, int64_t n) {
+    if (!h || n <= 0) return 0;
+    // every symbol but the first advances the M&M clock by >= sps - 0.1 samples
+    const double min_adv = h->lp.sps - 0.1;
+    int64_t bound = n;
+    if (min_adv > 0.5) {
+        const double b = std::ceil(static_cast<double>(n + kCarryMax) / min_adv) + 4.0;
+        if (b < static_cast<double>(n)) bound = static_cast<int64_t>(b);
+    }
+    return bound;
+}
+
+int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod **out) {
+    if (!p || !out) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    *out = nullptr;
+    if (n_streams <= 0) return fail(QPSK_ERR_ARGUMENT, "n_streams must be positive");
+    if (p->max_samples_per_call <= 0) return fail(QPSK_ERR_ARGUMENT, "max_samples_per_call must be positive");
+    auto *h = new qpsk_demod();
+    h->p = *p;
+    h->S = n_streams;
+    h->W = p->vector_lanes <= 1 ? 1 : p->vector_lanes;
+    if (h->W != 1 && h->W != 4 && h->W != 8 && h->W != 16) {
+        delete h;
+        return fail(QPSK_ERR_ARGUMENT, "vector_lanes must be 1, 4, 8 or 16");
+    }
+    std::string err;
+    int rc = design_loops(p->sample_rate, p->symbol_rate, p->rrc_alpha, p->rrc_span,
+                          p->symbol_sync_bandwidth, p->costas_loop_bandwidth, p->cfo_loop_bandwidth,
+                          &h->d, &err);
+    if (rc != QPSK_OK) {
+        delete h;
+        return fail(rc, err);
+    }
+    h->T = static_cast<int>(h->d.rrc_f32.size());
+    for (int k = 0; k < h->T && k < kMaxTapsSpecialised; ++k) h->taps.h[k] = h->d.rrc_f32[h->T - 1 - k];
+    h->lp.sps = h->d.mm_sps;
+    h->lp.kp = h->d.kp;
+    h->lp.ki = h->d.ki;
+    h->lp.c_alpha = h->d.costas_alpha;
+    h->lp.c_beta = h->d.costas_beta;
+    h->lp.differential = p->differential ? 1 : 0;
+    h->fp.beta = h->d.fll_beta;
+    h->fp.alpha = h->d.fll_alpha;
+    h->fp.max_freq = h->d.fll_max_freq;
+    h->fp.min_freq = -h->d.fll_max_freq;
+    h->fp.lanes = h->W;
+    for (int k = 0; k < kFllTaps; ++k) {
+        const int src = kFllTaps - 1 - k;
+        h->fp.lower_rev[2 * k] = h->d.fll_lower_iq[2 * src];
+        h->fp.lower_rev[2 * k + 1] = h->d.fll_lower_iq[2 * src + 1];
+        h->fp.upper_rev[2 * k] = h->d.fll_upper_iq[2 * src];
+        h->fp.upper_rev[2 * k + 1] = h->d.fll_upper_iq[2 * src + 1];
+    }
+
+    auto cleanup_fail = [&](int code) {
+        qpsk_demod_destroy(h);
+        return code;
+    };
+    if (hipSetDevice(p->device) != hipSuccess)
+        return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipSetDevice failed (no GPU?)"));
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+        return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipStreamCreate failed"));
+    h->own_stream = true;
+    for (auto &e : h->ev)
+        if (hipEventCreate(&e) != hipSuccess) return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipEventCreate"));
+
+    const int64_t S = n_streams;
+    h->n_max = p->max_samples_per_call;
+    h->mf_stride = ((kMfPrefix + h->n_max + 63) / 64) * 64;
+    h->syms_cap = qpsk_demod_max_symbols(h, h->n_max);
+    h->bits_words = (2 * h->syms_cap + 31) / 32 + 1;
+    const int H = h->T - 1;
+    if ((rc = dev_alloc(&h->d_hrev, h->T)) || (rc = dev_alloc(&h->d_hist[0], 2 * S * H)) ||
+        (rc = dev_alloc(&h->d_hist[1], 2 * S * H)) ||
+        (rc = dev_alloc(&h->d_mf, static_cast<size_t>(2 * S * h->mf_stride))) ||
+        (rc = dev_alloc(&h->d_carry, 2 * S * kCarryMax)) || (rc = dev_alloc(&h->d_state, S)) ||
+        (rc = dev_alloc(&h->d_fll_delay, 2 * S * 2 * kFllTaps)) ||
+        (rc = dev_alloc(&h->d_bits, static_cast<size_t>(S * h->bits_words))) ||
+        (rc = dev_alloc(&h->d_counts, 2 * S)) || (rc = dev_alloc(&h->d_lengths, S)))
+        return cleanup_fail(rc);
+    if (p->enable_fll && (rc = dev_alloc(&h->d_fll_out, static_cast<size_t>(2 * S * h->n_max))))
+        return cleanup_fail(rc);
+    if (hipHostMalloc(reinterpret_cast<void **>(&h->h_counts), 2 * S * sizeof(int64_t)) != hipSuccess)
+        return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipHostMalloc"));
+    std::vector<float> hrev(h->T);
+    for (int k = 0; k < h->T; ++k) hrev[k] = h->d.rrc_f32[h->T - 1 - k];
+    // Fresh instances: zero delay lines (FIRFilter.cs:50-51), M&M baseIndex = 1
+    // (MuellerMuller.cs:44), everything else zero.
+    std::vector<StreamState> st(S);
+    for (auto &x : st) {
+        std::memset(&x, 0, sizeof(x));
+        x.base = 1;
+    }
+    if (hipMemcpy(h->d_hrev, hrev.data(), h->T * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->d_state, st.data(), S * sizeof(StreamState), hipMemcpyHostToDevice) != hipSuccess ||
+        (H > 0 && hipMemset(h->d_hist[0], 0, 2 * S * H * sizeof(float)) != hipSuccess) ||
+        hipMemset(h->d_carry, 0, 2 * S * kCarryMax * sizeof(float)) != hipSuccess ||
+        hipMemset(h->d_fll_delay, 0, 2 * S * 2 * kFllTaps * sizeof(float)) != hipSuccess ||
+        hipMemset(h->d_mf, 0, static_cast<size_t>(2 * S * h->mf_stride) * sizeof(float)) != hipSuccess)
+        return cleanup_fail(fail(QPSK_ERR_DEVICE, "device init failed"));
+    *out = h;
+    return QPSK_OK;
+}
+
+int qpsk_demod_destroy(qpsk_demod *h) {
+    if (!h) return QPSK_OK;
+    if (h->stream) hipStreamSynchronize(h->stream);
+    hipFree(h->d_hrev);
+    hipFree(h->d_in);
+    hipFree(h->d_fll_out);
+    hipFree(h->d_hist[0]);
+    hipFree(h->d_hist[1]);
+    hipFree(h->d_mf);
+    hipFree(h->d_carry);
+    hipFree(h->d_state);
+    hipFree(h->d_fll_delay);
+    hipFree(h->d_bits);
+    hipFree(h->d_syms);
+    hipFree(h->d_counts);
+    hipFree(h->d_lengths);
+    if (h->h_counts) hipHostFree(h->h_counts);
+    for (auto &e : h->ev)
+        if (e) hipEventDestroy(e);
+    if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
+    delete h;
+    return QPSK_OK;
+}
+
+int qpsk_demod_set_stream(qpsk_demod *h, void *hip_stream) {
+    if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (hip_stream) {
+        if (h->own_stream) hipStreamDestroy(h->stream);
+        h->stream = static_cast<hipStream_t>(hip_stream);
+        h->own_stream = false;
+    } else if (!h->own_stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        h->own_stream = true;
+    }
+    return QPSK_OK;
+}
+
+int qpsk_demod_enable_timing(qpsk_demod *h, int32_t on) {
+    if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
+    h->timing = on != 0;
+    return QPSK_OK;
+}
+
+int qpsk_demod_stage_times(const qpsk_demod *h, float *ms, int32_t n) {
+    if (!h || !ms) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    const int k = std::min<int32_t>(n, 4);
+    for (int i = 0; i < k; ++i) ms[i] = h->stage_ms[i];
+    return k;
+}
+
+int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t stride_floats,
+                       int64_t n_samples, const int64_t *lengths, int32_t mem, uint8_t *bits,
+                       int64_t bits_stride_bytes, int64_t *n_bits, float *syms,
+                       int64_t syms_stride_floats, int64_t *n_syms) {
+    if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
+    if (mode != QPSK_MODE_DEMODULATE && mode != QPSK_MODE_CONSTELLATION)
+        return fail(QPSK_ERR_ARGUMENT, "unknown mode");
+    if (mem != QPSK_MEM_HOST && mem != QPSK_MEM_DEVICE) return fail(QPSK_ERR_ARGUMENT, "unknown mem");
+    const int S = h->S;
+    int64_t n_call = 0;
+    if (lengths) {
+        for (int s = 0; s < S; ++s) {
+            if (lengths[s] < 0) return fail(QPSK_ERR_ARGUMENT, "negative length");
+            n_call = std::max(n_call, lengths[s]);
+        }
+    } else {
+        if (n_samples < 0) return fail(QPSK_ERR_ARGUMENT, "negative n_samples");
+        n_call = n_samples;
+    }
+    if (n_call > h->n_max) return fail(QPSK_ERR_CAPACITY, "call longer than max_samples_per_call");
+    if (n_call > 0 && !iq) return fail(QPSK_ERR_ARGUMENT_NULL, "SamplesIQ is null");
+    if (n_call > 0 && stride_floats < 2 * n_call) return fail(QPSK_ERR_ARGUMENT, "stride too small");
+    if (mode == QPSK_MODE_DEMODULATE && (!bits || !n_bits))
+        return fail(QPSK_ERR_ARGUMENT_NULL, "bits / n_bits required");
+    if (mode == QPSK_MODE_CONSTELLATION && (!syms || !n_syms))
+        return fail(QPSK_ERR_ARGUMENT_NULL, "syms / n_syms required");
+    const int64_t max_sym = qpsk_demod_max_symbols(h, n_call);
+    if (bits && bits_stride_bytes < ((2 * max_sym + 7) / 8))
+        return fail(QPSK_ERR_ARGUMENT, "bits_stride_bytes smaller than 2*max_symbols/8");
+    if (syms && syms_stride_floats < 2 * max_sym)
+        return fail(QPSK_ERR_ARGUMENT, "syms_stride_floats smaller than 2*max_symbols");
+    int rc;
+    if (syms && !h->d_syms) {
+        if ((rc = dev_alloc(&h->d_syms, static_cast<size_t>(2 * S * h->syms_cap)))) return rc;
+    }
+    hipStream_t st = h->stream;
+    HIP_TRY(hipSetDevice(h->p.device));
+    if (h->timing) HIP_TRY(hipEventRecord(h->ev[0], st));
+
+    // ---- input -----------------------------------------------------------
+    const float *x = iq;
+    int64_t x_stride = stride_floats / 2;   // float2 units
+    if (n_call > 0 && mem == QPSK_MEM_HOST) {
+        if (!h->d_in && (rc = dev_alloc(&h->d_in, static_cast<size_t>(2 * S * h->n_max)))) return rc;
+        HIP_TRY(hipMemcpy2DAsync(h->d_in, 2 * h->n_max * sizeof(float), iq, stride_floats * sizeof(float),
+                                 2 * n_call * sizeof(float), S, hipMemcpyHostToDevice, st));
+        x = h->d_in;
+        x_stride = h->n_max;
+    } else if (n_call > 0 && (stride_floats & 1)) {
+        return fail(QPSK_ERR_ARGUMENT, "device stride_floats must be even");
+    }
+    const int64_t *d_len = nullptr;
+    if (lengths) {
+        HIP_TRY(hipMemcpyAsync(h->d_lengths, lengths, S * sizeof(int64_t), hipMemcpyHostToDevice, st));
+        d_len = h->d_lengths;
+    }
+
+    // ---- FLL (Band-Edge Filter.cs:64-87), README order FLL -> MF ------------
+    if (h->p.enable_fll && n_call > 0) {
+        FllArgs fa{};
+        fa.x = x; fa.x_stride = x_stride;
+        fa.y = h->d_fll_out; fa.y_stride = h->n_max;
+        fa.delay = h->d_fll_delay;
+        fa.lengths = d_len; fa.n = n_call;
+        fa.state = h->d_state; fa.S = S;
+        launch_fll(fa, h->fp, st);
+        x = h->d_fll_out;
+        x_stride = h->n_max;
+    }
+    if (h->timing) HIP_TRY(hipEventRecord(h->ev[1], st));
+
+    // ---- matched filter (QPSKDeModulator.cs:360) ----------------------------
+    FirArgs fa{};
+    fa.x = x; fa.x_stride = x_stride;
+    fa.hist = h->d_hist[h->hist_cur];
+    fa.lengths = d_len; fa.n = n_call;
+    fa.y = h->d_mf; fa.y_stride = h->mf_stride; fa.y_offset = kMfPrefix;
+    if (n_call > 0) {
+        launch_fir(fa, h->taps, h->d_hrev, h->T, h->W, S, n_call, st);
+        launch_fir_hist(fa, h->d_hist[h->hist_cur ^ 1], h->T - 1, S, st);
+        h->hist_cur ^= 1;
+    }
+    if (h->timing) HIP_TRY(hipEventRecord(h->ev[2], st));
+
+    // ---- symbol sync + Costas + decode (QPSKDeModulator.cs:364-408) --------
+    LoopArgs la{};
+    la.mf = h->d_mf; la.mf_stride = h->mf_stride;
+    la.carry = h->d_carry;
+    la.lengths = d_len; la.n = n_call;
+    la.state = h->d_state;
+    la.bits = mode == QPSK_MODE_DEMODULATE ? h->d_bits : nullptr;
+    la.bits_stride_words = h->bits_words;
+    la.bits_cap_words = h->bits_words;
+    la.n_bits = h->d_counts;
+    la.syms = syms ? h->d_syms : nullptr;
+    la.syms_stride = h->syms_cap;
+    la.syms_cap = h->syms_cap;
+    la.n_syms = h->d_counts + S;
+    la.S = S;
+    launch_loop(la, h->lp, mode, 64, st);
+    HIP_TRY(hipGetLastError());
+    if (h->timing) HIP_TRY(hipEventRecord(h->ev[3], st));
+
+    // ---- outputs -----------------------------------------------------------
+    const hipMemcpyKind kind = mem == QPSK_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    const int64_t bytes_row = (2 * max_sym + 7) / 8;
+    if (bits && bytes_row > 0)
+        HIP_TRY(hipMemcpy2DAsync(bits, bits_stride_bytes, h->d_bits, h->bits_words * 4, bytes_row, S, kind, st));
+    if (syms && max_sym > 0)
+        HIP_TRY(hipMemcpy2DAsync(syms, syms_stride_floats * sizeof(float), h->d_syms,
+                                 2 * h->syms_cap * sizeof(float), 2 * max_sym * sizeof(float), S, kind, st));
+    if (mem == QPSK_MEM_HOST) {
+        HIP_TRY(hipMemcpyAsync(h->h_counts, h->d_counts, 2 * S * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (n_bits) std::memcpy(n_bits, h->h_counts, S * sizeof(int64_t));
+        if (n_syms) std::memcpy(n_syms, h->h_counts + S, S * sizeof(int64_t));
+    } else {
+        if (n_bits) HIP_TRY(hipMemcpyAsync(n_bits, h->d_counts, S * sizeof(int64_t), kind, st));
+        if (n_syms) HIP_TRY(hipMemcpyAsync(n_syms, h->d_counts + S, S * sizeof(int64_t), kind, st));
+    }
+    if (h->timing) {
+        HIP_TRY(hipEventSynchronize(h->ev[3]));
+        HIP_TRY(hipEventElapsedTime(&h->stage_ms[0], h->ev[0], h->ev[1]));
+        HIP_TRY(hipEventElapsedTime(&h->stage_ms[1], h->ev[1], h->ev[2]));
+        HIP_TRY(hipEventElapsedTime(&h->stage_ms[2], h->ev[2], h->ev[3]));
+        HIP_TRY(hipEventElapsedTime(&h->stage_ms[3], h->ev[0], h->ev[3]));
+    }
+    return QPSK_OK;
+}
+
+int qpsk_demod_rrc_taps(const qpsk_demod *h, float *taps, int32_t cap) {
+    if (!h || !taps) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    if (cap < h->T) return fail(QPSK_ERR_ARGUMENT, "cap too small");
+    std::memcpy(taps, h->d.rrc_f32.data(), h->T * sizeof(float));
+    return h->T;
+}
+
+int qpsk_demod_gains(const qpsk_demod *h, double *mm_sps, double *kp, double *ki,
+                     double *costas_alpha, double *costas_beta) {
+    if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
+    if (mm_sps) *mm_sps = h->d.mm_sps;
+    if (kp) *kp = h->d.kp;
+    if (ki) *ki = h->d.ki;
+    if (costas_alpha) *costas_alpha = h->d.costas_alpha;
+    if (costas_beta) *costas_beta = h->d.costas_beta;
+    return QPSK_OK;
+}
+
+int qpsk_demod_fll_taps(const qpsk_demod *h, float *lower_iq, float *upper_iq, int32_t cap_floats) {
+    if (!h || !lower_iq || !upper_iq) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    const int n = 2 * kFllTaps;
+    if (cap_floats < n) return fail(QPSK_ERR_ARGUMENT, "cap too small");
+    std::memcpy(lower_iq, h->d.fll_lower_iq.data(), n * sizeof(float));
+    std::memcpy(upper_iq, h->d.fll_upper_iq.data(), n * sizeof(float));
+    return n;
+}
+
+int qpsk_demod_design(const qpsk_demod_params *p, float *rrc_taps, int32_t cap, double *gains,
+                      float *fll_lower_iq, float *fll_upper_iq) {
+    if (!p) return fail(QPSK_ERR_ARGUMENT_NULL, "null params");
+    LoopDesign d;
+    std::string err;
+    int rc = design_loops(p->sample_rate, p->symbol_rate, p->rrc_alpha, p->rrc_span,
+                          p->symbol_sync_bandwidth, p->costas_loop_bandwidth, p->cfo_loop_bandwidth,
+                          &d, &err);
+    if (rc != QPSK_OK) return fail(rc, err);
+    const int T = static_cast<int>(d.rrc_f32.size());
+    if (rrc_taps) {
+        if (cap < T) return fail(QPSK_ERR_ARGUMENT, "cap too small");
+        std::memcpy(rrc_taps, d.rrc_f32.data(), T * sizeof(float));
+    }
+    if (gains) {
+        gains[0] = d.mm_sps; gains[1] = d.kp; gains[2] = d.ki;
+        gains[3] = d.costas_alpha; gains[4] = d.costas_beta;
+    }
+    if (fll_lower_iq) std::memcpy(fll_lower_iq, d.fll_lower_iq.data(), 2 * kFllTaps * sizeof(float));
+    if (fll_upper_iq) std::memcpy(fll_upper_iq, d.fll_upper_iq.data(), 2 * kFllTaps * sizeof(float));
+    return T;
+}
+
+int64_t qpsk_demod_state_bytes(const qpsk_demod *h) {
+    if (!h) return 0;
+    const int64_t S = h->S, H = h->T - 1;
+    return S * (static_cast<int64_t>(sizeof(StreamState)) + 8 * kCarryMax + 8 * H + 8 * 2 * kFllTaps);
+}
+
+int qpsk_demod_get_state(const qpsk_demod *h, void *host_buf) {
+    if (!h || !host_buf) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    const int64_t S = h->S, H = h->T - 1;
+    char *p = static_cast<char *>(host_buf);
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipMemcpy(p, h->d_state, S * sizeof(StreamState), hipMemcpyDeviceToHost));
+    p += S * sizeof(StreamState);
+    HIP_TRY(hipMemcpy(p, h->d_carry, S * 8 * kCarryMax, hipMemcpyDeviceToHost));
+    p += S * 8 * kCarryMax;
+    if (H > 0) HIP_TRY(hipMemcpy(p, h->d_hist[h->hist_cur], S * 8 * H, hipMemcpyDeviceToHost));
+    p += S * 8 * H;
+    HIP_TRY(hipMemcpy(p, h->d_fll_delay, S * 8 * 2 * kFllTaps, hipMemcpyDeviceToHost));
+    return QPSK_OK;
+}
+
+int qpsk_demod_set_state(qpsk_demod *h, const void *host_buf) {
+    if (!h || !host_buf) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    const int64_t S = h->S, H = h->T - 1;
+    const char *p = static_cast<const char *>(host_buf);
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipMemcpy(h->d_state, p, S * sizeof(StreamState), hipMemcpyHostToDevice));
+    p += S * sizeof(StreamState);
+    HIP_TRY(hipMemcpy(h->d_carry, p, S * 8 * kCarryMax, hipMemcpyHostToDevice));
+    p += S * 8 * kCarryMax;
+    if (H > 0) HIP_TRY(hipMemcpy(h->d_hist[h->hist_cur], p, S * 8 * H, hipMemcpyHostToDevice));
+    p += S * 8 * H;
+    HIP_TRY(hipMemcpy(h->d_fll_delay, p, S * 8 * 2 * kFllTaps, hipMemcpyHostToDevice));
+    return QPSK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,53 @@
+// qpsk_state.h -- per-stream loop state kept in HBM between process() calls,
+// and the uniform launch parameters of the loop kernels.
+//
+// One StreamState per stream = the private fields of one reference
+// QPSKDeModulator instance:
+//   MuellerMuller.cs:24-36      baseIndex, mu, ncoIntegral, prev sample/decision
+//   CostasLoopQpsk.cs:25-27     theta, freq
+//   QPSKDeModulator.cs:72-73    differential-decoder previous decision
+//   Band-Edge Filter.cs:25-26   FLL phase, freq (+ the 40-sample delay line, kept
+//                               in its own array)
+// The M&M sample queue (MuellerMuller.cs:32-36) is kept as the count of
+// retained matched-filter samples plus those samples in a carry array.
+#pragma once
+#include <cstdint>
+
+namespace qpsk {
+
+constexpr int kCarryMax = 64;      // retained M&M samples between calls (normally 3)
+constexpr int kMfPrefix = 64;      // MF buffer prefix that receives the carry
+constexpr int kFllTaps = 40;       // QPSKDeModulator.cs:35
+constexpr int kMaxTapsSpecialised = 260;
+
+struct alignas(16) StreamState {
+    double mu;          // MuellerMuller.mu
+    double integ;       // MuellerMuller.ncoIntegral
+    double theta;       // CostasLoopQpsk.theta
+    double freq;        // CostasLoopQpsk.freq
+    int32_t base;       // MuellerMuller.baseIndex (relative to the retained queue)
+    int32_t has_prev;   // MuellerMuller.hasPrev
+    float psi, psq;     // MuellerMuller.prevSample
+    float pdi, pdq;     // MuellerMuller.prevDecision
+    int32_t carry_n;    // retained queue length (_bufCount after the last call)
+    int32_t diff_have;  // QPSKDeModulator._diffHavePrev
+    float diff_pi, diff_pq;
+    float fll_phase, fll_freq;
+    int32_t fll_pos;    // FLL delay-line write position
+    int32_t error;      // sticky: 1 = carry overflow
+};
+
+struct LoopParams {
+    double sps, kp, ki;            // MuellerMuller
+    double c_alpha, c_beta;        // CostasLoopQpsk
+    int32_t differential;
+};
+
+struct FllParams {
+    float beta, alpha, max_freq, min_freq;
+    float lower_rev[2 * kFllTaps]; // interleaved complex taps, reversed
+    float upper_rev[2 * kFllTaps]; // (ComplexFIRFilter ctor, FIRFilter.cs:43-48)
+    int32_t lanes;
+};
+
+}  // namespace qpsk

@@ -1,0 +1,454 @@
+"""Python binding of libqpsk_demod.so (the C ABI in include/qpsk_demod.h).
+
+Mirrors the reference C# API so the parity tests read like the reference's own
+usage (testAtDataLevel.cs, ModDemodOverSDR.cs):
+
+    QPSKDeModulator(SampleRate, SymbolRate, RrcAlpha=0.9, rrcSpan=6, ...)
+        .DeModulate(samples) -> str            (QPSKDeModulator.cs:339-425)
+        .deModulateConstellation(samples)      (:427-455)
+        .DeModulateBytes(samples, start, end)  (:169-259)
+        .DeModulateTextUtf8(samples, ...)      (:262-277)
+
+and exposes the batched handle (`BatchDemodulator`) that one MI355X runs over
+thousands of streams.  There is no CPU fallback: if the HIP library is missing
+or no GPU is present, every compute call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(_PKG, "_build", "libqpsk_demod.so")
+
+QPSK_OK = 0
+QPSK_ERR_ARGUMENT = -1
+QPSK_ERR_ARGUMENT_NULL = -2
+QPSK_ERR_OUT_OF_RANGE = -3
+QPSK_ERR_DEVICE = -4
+QPSK_ERR_CAPACITY = -5
+QPSK_ERR_STATE = -6
+MEM_HOST = 0
+MEM_DEVICE = 1
+MODE_DEMODULATE = 0
+MODE_CONSTELLATION = 1
+
+_i64p = C.POINTER(C.c_int64)
+_u8p = C.POINTER(C.c_uint8)
+_f32p = C.POINTER(C.c_float)
+_f64p = C.POINTER(C.c_double)
+
+
+class DemodParams(C.Structure):
+    _fields_ = [
+        ("sample_rate", C.c_int32),
+        ("symbol_rate", C.c_int32),
+        ("rrc_alpha", C.c_float),
+        ("rrc_span", C.c_int32),
+        ("symbol_sync_bandwidth", C.c_double),
+        ("costas_loop_bandwidth", C.c_double),
+        ("cfo_loop_bandwidth", C.c_double),
+        ("differential", C.c_int32),
+        ("enable_fll", C.c_int32),
+        ("vector_lanes", C.c_int32),
+        ("device", C.c_int32),
+        ("max_samples_per_call", C.c_int64),
+        ("reserved", C.c_int32 * 8),
+    ]
+
+
+class SynthParams(C.Structure):
+    _fields_ = [
+        ("sample_rate", C.c_int32),
+        ("symbol_rate", C.c_int32),
+        ("rrc_alpha", C.c_double),
+        ("rrc_span", C.c_int32),
+        ("differential", C.c_int32),
+        ("seed", C.c_uint64),
+        ("lo_ppm", C.c_double),
+        ("cfo_hz", C.c_double),
+        ("multipath", C.c_int32),
+        ("esn0_db", C.c_double),
+        ("reserved", C.c_int32 * 8),
+    ]
+
+
+class QPSKError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load the HIP library; raise loudly if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise QPSKError(f"{LIB_PATH} missing: run `make -C qpsk-modulator-demodulator_amd` "
+                        "(there is no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    L.qpsk_abi_version.restype = C.c_int
+    L.qpsk_last_error.restype = C.c_char_p
+    L.qpsk_demod_params_init.argtypes = [C.POINTER(DemodParams), C.c_int32, C.c_int32]
+    L.qpsk_demod_create.argtypes = [C.POINTER(DemodParams), C.c_int32, C.POINTER(C.c_void_p)]
+    L.qpsk_demod_destroy.argtypes = [C.c_void_p]
+    L.qpsk_demod_set_stream.argtypes = [C.c_void_p, C.c_void_p]
+    L.qpsk_demod_process.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64, C.c_int64,
+                                     _i64p, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p,
+                                     C.c_void_p, C.c_int64, C.c_void_p]
+    L.qpsk_demod_max_symbols.argtypes = [C.c_void_p, C.c_int64]
+    L.qpsk_demod_max_symbols.restype = C.c_int64
+    L.qpsk_tsc_find.argtypes = [_u8p, C.c_int64, C.c_char_p]
+    L.qpsk_tsc_find.restype = C.c_int64
+    L.qpsk_demod_enable_timing.argtypes = [C.c_void_p, C.c_int32]
+    L.qpsk_demod_stage_times.argtypes = [C.c_void_p, _f32p, C.c_int32]
+    L.qpsk_demod_rrc_taps.argtypes = [C.c_void_p, _f32p, C.c_int32]
+    L.qpsk_demod_gains.argtypes = [C.c_void_p] + [_f64p] * 5
+    L.qpsk_demod_fll_taps.argtypes = [C.c_void_p, _f32p, _f32p, C.c_int32]
+    L.qpsk_demod_state_bytes.argtypes = [C.c_void_p]
+    L.qpsk_demod_state_bytes.restype = C.c_int64
+    L.qpsk_demod_get_state.argtypes = [C.c_void_p, C.c_void_p]
+    L.qpsk_demod_set_state.argtypes = [C.c_void_p, C.c_void_p]
+    L.qpsk_framer_create.argtypes = [C.c_int32, _u8p, C.c_int32, _u8p, C.c_int32, C.c_int64,
+                                     C.POINTER(C.c_void_p)]
+    L.qpsk_framer_destroy.argtypes = [C.c_void_p]
+    L.qpsk_framer_set_markers.argtypes = [C.c_void_p, _u8p, C.c_int32, _u8p, C.c_int32]
+    L.qpsk_demod_design.argtypes = [C.POINTER(DemodParams), _f32p, C.c_int32, _f64p, _f32p, _f32p]
+    L.qpsk_framer_push.argtypes = [C.c_void_p, _u8p, C.c_int64, _i64p, _i64p, _u8p, C.c_int64,
+                                   _i64p]
+    L.qpsk_synth_params_init.argtypes = [C.POINTER(SynthParams), C.c_int32, C.c_int32]
+    L.qpsk_synth_generate.argtypes = [C.POINTER(SynthParams), C.c_int32, C.c_void_p, C.c_int32,
+                                      C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]
+    _lib = L
+    return L
+
+
+EXPORTED_SYMBOLS = [
+    "qpsk_abi_version", "qpsk_last_error", "qpsk_demod_params_init", "qpsk_demod_create",
+    "qpsk_demod_destroy", "qpsk_demod_set_stream", "qpsk_demod_process", "qpsk_demod_max_symbols",
+    "qpsk_tsc_find", "qpsk_demod_enable_timing", "qpsk_demod_stage_times", "qpsk_demod_rrc_taps",
+    "qpsk_demod_gains", "qpsk_demod_fll_taps", "qpsk_demod_state_bytes", "qpsk_demod_get_state",
+    "qpsk_demod_set_state", "qpsk_demod_design", "qpsk_framer_create", "qpsk_framer_destroy",
+    "qpsk_framer_set_markers", "qpsk_framer_push",
+    "qpsk_synth_params_init", "qpsk_synth_generate",
+]
+
+_EXC = {
+    QPSK_ERR_ARGUMENT: ValueError,
+    QPSK_ERR_ARGUMENT_NULL: ValueError,
+    QPSK_ERR_OUT_OF_RANGE: ValueError,
+    QPSK_ERR_CAPACITY: ValueError,
+}
+
+
+def _check(rc):
+    if rc < 0:
+        msg = lib().qpsk_last_error().decode(errors="replace")
+        raise _EXC.get(rc, QPSKError)(f"qpsk error {rc}: {msg}")
+    return rc
+
+
+def params(sample_rate, symbol_rate, rrc_alpha=0.9, rrc_span=6, symbol_sync_bandwidth=0.0001,
+           costas_loop_bandwidth=120.0, cfo_loop_bandwidth=None, differential=True,
+           enable_fll=False, vector_lanes=8, device=0, max_samples_per_call=1 << 20):
+    p = DemodParams()
+    lib().qpsk_demod_params_init(C.byref(p), int(sample_rate), int(symbol_rate))
+    p.rrc_alpha = float(np.float32(rrc_alpha))
+    p.rrc_span = int(rrc_span)
+    p.symbol_sync_bandwidth = float(symbol_sync_bandwidth)
+    p.costas_loop_bandwidth = float(costas_loop_bandwidth)
+    if cfo_loop_bandwidth is not None:
+        p.cfo_loop_bandwidth = float(cfo_loop_bandwidth)
+    p.differential = 1 if differential else 0
+    p.enable_fll = 1 if enable_fll else 0
+    p.vector_lanes = int(vector_lanes)
+    p.device = int(device)
+    p.max_samples_per_call = int(max_samples_per_call)
+    return p
+
+
+def unpack_bits(row: np.ndarray, n_bits: int) -> str:
+    """Packed MSB-first bits -> '0'/'1' string (the reference's bit strings)."""
+    if n_bits <= 0:
+        return ""
+    b = np.unpackbits(np.asarray(row, dtype=np.uint8)[: (n_bits + 7) // 8])[:n_bits]
+    return (b + ord("0")).astype(np.uint8).tobytes().decode()
+
+
+def pack_bits(bits: str) -> np.ndarray:
+    a = np.frombuffer(bits.encode(), dtype=np.uint8) - ord("0")
+    return np.packbits(a)
+
+
+class BatchDemodulator:
+    """A batch of S independent reference demodulators on one MI355X."""
+
+    def __init__(self, n_streams: int, p: DemodParams):
+        self.S = int(n_streams)
+        self.p = p
+        h = C.c_void_p()
+        _check(lib().qpsk_demod_create(C.byref(p), self.S, C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().qpsk_demod_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, hip_stream_ptr: int | None):
+        _check(lib().qpsk_demod_set_stream(self._h, C.c_void_p(hip_stream_ptr or 0)))
+
+    def max_symbols(self, n: int) -> int:
+        return int(lib().qpsk_demod_max_symbols(self._h, int(n)))
+
+    def enable_timing(self, on=True):
+        _check(lib().qpsk_demod_enable_timing(self._h, 1 if on else 0))
+
+    def stage_times(self):
+        ms = (C.c_float * 4)()
+        lib().qpsk_demod_stage_times(self._h, ms, 4)
+        return {"fll": ms[0], "fir": ms[1], "loop": ms[2], "total": ms[3]}
+
+    def rrc_taps(self):
+        out = np.zeros(4096, dtype=np.float32)
+        n = _check(lib().qpsk_demod_rrc_taps(self._h, out.ctypes.data_as(_f32p), 4096))
+        return out[:n].copy()
+
+    def gains(self):
+        v = [C.c_double() for _ in range(5)]
+        _check(lib().qpsk_demod_gains(self._h, *[C.byref(x) for x in v]))
+        return dict(zip(["mm_sps", "kp", "ki", "costas_alpha", "costas_beta"], [x.value for x in v]))
+
+    def fll_taps(self):
+        lo = np.zeros(80, dtype=np.float32)
+        up = np.zeros(80, dtype=np.float32)
+        _check(lib().qpsk_demod_fll_taps(self._h, lo.ctypes.data_as(_f32p), up.ctypes.data_as(_f32p), 80))
+        return lo, up
+
+    def get_state(self) -> bytes:
+        n = lib().qpsk_demod_state_bytes(self._h)
+        buf = C.create_string_buffer(n)
+        _check(lib().qpsk_demod_get_state(self._h, buf))
+        return buf.raw
+
+    def set_state(self, blob: bytes):
+        buf = C.create_string_buffer(blob, len(blob))
+        _check(lib().qpsk_demod_set_state(self._h, buf))
+
+    # ---- host path --------------------------------------------------------
+    def process(self, iq: np.ndarray, mode=MODE_DEMODULATE, lengths=None, want_syms=False):
+        """iq: [S, 2n] float32 host array.  Returns (bits [S, B] uint8, n_bits [S],
+        syms [S, 2M] float32 or None, n_syms [S])."""
+        iq = np.ascontiguousarray(iq, dtype=np.float32)
+        if iq.ndim != 2 or iq.shape[0] != self.S:
+            raise ValueError("iq must be [n_streams, 2*n]")
+        if iq.shape[1] & 1:
+            raise ValueError("Samples must be interleaved IQ with even length.")
+        n = iq.shape[1] // 2
+        if lengths is not None:
+            lengths = np.ascontiguousarray(lengths, dtype=np.int64)
+            nmax = int(lengths.max()) if lengths.size else 0
+        else:
+            nmax = n
+        ms = max(self.max_symbols(nmax), 1)
+        bstride = (2 * ms + 7) // 8 + 8
+        bits = np.zeros((self.S, bstride), dtype=np.uint8)
+        n_bits = np.zeros(self.S, dtype=np.int64)
+        n_syms = np.zeros(self.S, dtype=np.int64)
+        syms = np.zeros((self.S, 2 * ms), dtype=np.float32) if (want_syms or mode == MODE_CONSTELLATION) else None
+        _check(lib().qpsk_demod_process(
+            self._h, int(mode), iq.ctypes.data if iq.size else None, max(iq.shape[1], 2 * nmax), n,
+            lengths.ctypes.data_as(_i64p) if lengths is not None else None, MEM_HOST,
+            bits.ctypes.data if mode == MODE_DEMODULATE else None, bstride,
+            n_bits.ctypes.data if mode == MODE_DEMODULATE else None,
+            syms.ctypes.data if syms is not None else None, 2 * ms,
+            n_syms.ctypes.data))
+        return bits, n_bits, syms, n_syms
+
+    # ---- device path (torch tensors resident in HBM) ---------------------
+    def process_device(self, iq_dev, n, bits_dev, n_bits_dev, mode=MODE_DEMODULATE,
+                       syms_dev=None, n_syms_dev=None):
+        """All arguments are torch CUDA tensors; stream-ordered on the handle's
+        stream (bind torch's stream with set_stream first)."""
+        bstride = bits_dev.stride(0) * bits_dev.element_size()
+        sstride = syms_dev.stride(0) if syms_dev is not None else 0
+        _check(lib().qpsk_demod_process(
+            self._h, int(mode), iq_dev.data_ptr(), iq_dev.stride(0), int(n), None, MEM_DEVICE,
+            bits_dev.data_ptr() if bits_dev is not None else None, bstride,
+            n_bits_dev.data_ptr() if n_bits_dev is not None else None,
+            syms_dev.data_ptr() if syms_dev is not None else None, sstride,
+            n_syms_dev.data_ptr() if n_syms_dev is not None else None))
+
+
+def design(p: DemodParams):
+    """Constructor math without a GPU: (rrc taps, gains dict, fll lower, fll upper)."""
+    taps = np.zeros(4096, dtype=np.float32)
+    g = (C.c_double * 5)()
+    lo = np.zeros(80, dtype=np.float32)
+    up = np.zeros(80, dtype=np.float32)
+    n = _check(lib().qpsk_demod_design(C.byref(p), taps.ctypes.data_as(_f32p), 4096, g,
+                                       lo.ctypes.data_as(_f32p), up.ctypes.data_as(_f32p)))
+    gains = dict(zip(["mm_sps", "kp", "ki", "costas_alpha", "costas_beta"], list(g)))
+    return taps[:n].copy(), gains, lo, up
+
+
+def tsc_find(bits_row: np.ndarray, n_bits: int, tsc: str | None) -> int:
+    row = np.ascontiguousarray(bits_row, dtype=np.uint8)
+    return int(lib().qpsk_tsc_find(row.ctypes.data_as(_u8p), int(n_bits),
+                                    tsc.encode() if tsc else None))
+
+
+class Framer:
+    """Batched DeModulateBytes framer (QPSKDeModulator.cs:169-259)."""
+
+    def __init__(self, n_streams, start: bytes, end: bytes, ring_capacity=300_000_000):
+        if len(start) == 0:
+            raise ValueError("startMarker cannot be empty.")
+        if len(end) == 0:
+            raise ValueError("endMarker cannot be empty.")
+        self.S = n_streams
+        s = np.frombuffer(start, dtype=np.uint8).copy()
+        e = np.frombuffer(end, dtype=np.uint8).copy()
+        h = C.c_void_p()
+        _check(lib().qpsk_framer_create(n_streams, s.ctypes.data_as(_u8p), s.size,
+                                        e.ctypes.data_as(_u8p), e.size, int(ring_capacity),
+                                        C.byref(h)))
+        self._h = h
+
+    def set_markers(self, start: bytes, end: bytes):
+        if len(start) == 0:
+            raise ValueError("startMarker cannot be empty.")
+        if len(end) == 0:
+            raise ValueError("endMarker cannot be empty.")
+        s = np.frombuffer(start, dtype=np.uint8).copy()
+        e = np.frombuffer(end, dtype=np.uint8).copy()
+        _check(lib().qpsk_framer_set_markers(self._h, s.ctypes.data_as(_u8p), s.size,
+                                             e.ctypes.data_as(_u8p), e.size))
+
+    def push(self, bits: np.ndarray, n_bits, offsets=None, payload_cap=1 << 16):
+        bits = np.ascontiguousarray(bits, dtype=np.uint8)
+        n_bits = np.ascontiguousarray(n_bits, dtype=np.int64)
+        off = np.ascontiguousarray(offsets if offsets is not None else np.zeros(self.S), dtype=np.int64)
+        pay = np.zeros((self.S, payload_cap), dtype=np.uint8)
+        npay = np.zeros(self.S, dtype=np.int64)
+        _check(lib().qpsk_framer_push(self._h, bits.ctypes.data_as(_u8p), bits.shape[1],
+                                      off.ctypes.data_as(_i64p), n_bits.ctypes.data_as(_i64p),
+                                      pay.ctypes.data_as(_u8p), payload_cap,
+                                      npay.ctypes.data_as(_i64p)))
+        return [bytes(pay[s, : min(int(npay[s]), payload_cap)]) for s in range(self.S)]
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().qpsk_framer_destroy(self._h)
+            self._h = None
+
+
+class QPSKDeModulator:
+    """Single-stream mirror of the reference class (QPSKDeModulator.cs:11-457),
+    backed by a 1-stream batch on the GPU."""
+
+    def __init__(self, SampleRate, SymbolRate, RrcAlpha=0.9, rrcSpan=6, SymbolSyncBandwith=0.0001,
+                 CostasLoopBandwith=120.0, CFOLoopBandwith=None, differentialEncoding=True,
+                 tsc=None, enable_fll=False, vector_lanes=8, device=0,
+                 max_samples_per_call=1 << 20, ring_capacity=300_000_000):
+        p = params(SampleRate, SymbolRate, RrcAlpha, rrcSpan, SymbolSyncBandwith, CostasLoopBandwith,
+                   CFOLoopBandwith, differentialEncoding, enable_fll, vector_lanes, device,
+                   max_samples_per_call)
+        self._b = BatchDemodulator(1, p)
+        self._tsc = None if (tsc is None or tsc.strip() == "") else tsc   # :21
+        self._framer = None
+        self._framer_key = None
+        self._ring_capacity = ring_capacity
+
+    def _demod_packed(self, samples):
+        x = np.ascontiguousarray(samples, dtype=np.float32).reshape(-1)
+        if x.size & 1:
+            raise ValueError("Samples must be interleaved IQ with even length.")   # :347-348
+        if x.size == 0:
+            return np.zeros((1, 1), np.uint8), 0, 0                               # :350-351
+        bits, nb, _, _ = self._b.process(x[None, :])
+        n = int(nb[0])
+        start = 0
+        if self._tsc is not None:                                                 # :413-422
+            start = tsc_find(bits[0], n, self._tsc)
+            if start < 0:
+                return bits, n, -1
+        return bits, n, start
+
+    def DeModulate(self, samples) -> str:
+        if samples is None:
+            raise ValueError("SamplesIQ")                                         # ArgumentNull :341
+        bits, n, start = self._demod_packed(samples)
+        if start < 0 or n == 0:
+            return ""
+        return unpack_bits(bits[0], n)[start:]
+
+    def deModulateConstellation(self, samples) -> np.ndarray:
+        if samples is None:
+            raise ValueError("SamplesIQ")
+        x = np.ascontiguousarray(samples, dtype=np.float32).reshape(-1)
+        if x.size & 1:
+            raise ValueError("Samples must be interleaved IQ with even length.")   # :430
+        _, _, syms, ns = self._b.process(x[None, :], mode=MODE_CONSTELLATION)
+        return syms[0, : 2 * int(ns[0])].copy()
+
+    def DeModulateBytes(self, samples, startMarker: bytes, endMarker: bytes) -> bytes:
+        if len(startMarker) == 0:
+            raise ValueError("startMarker cannot be empty.")                      # :174
+        if len(endMarker) == 0:
+            raise ValueError("endMarker cannot be empty.")                        # :175
+        key = (bytes(startMarker), bytes(endMarker))
+        if self._framer is None:
+            self._framer = Framer(1, key[0], key[1], self._ring_capacity)
+        elif self._framer_key != key:
+            self._framer.set_markers(key[0], key[1])   # per-call markers, state kept
+        self._framer_key = key
+        bits, n, start = self._demod_packed(samples)
+        if start < 0 or n - start <= 0:
+            return b""
+        out = self._framer.push(bits, np.array([n], np.int64), np.array([start], np.int64))
+        return out[0]
+
+    def DeModulateTextUtf8(self, samples, startMarker="\u0002", endMarker="\u0003") -> str:
+        p = self.DeModulateBytes(samples, startMarker.encode("utf-8"), endMarker.encode("utf-8"))
+        return p.decode("utf-8", errors="replace") if p else ""
+
+
+def synth_generate(n_streams, n_samples, sample_rate, symbol_rate, rrc_alpha=float(np.float32(0.4)),
+                   rrc_span=8, seed=0x5159534B, lo_ppm=1.0, cfo_hz=0.0, multipath=False,
+                   esn0_db=None, differential=True, device=0, stream=None, out=None, tx_bits=None):
+    """Batched synthetic baseband straight into HBM (torch tensors)."""
+    import torch
+    p = SynthParams()
+    lib().qpsk_synth_params_init(C.byref(p), int(sample_rate), int(symbol_rate))
+    p.rrc_alpha = float(rrc_alpha)
+    p.rrc_span = int(rrc_span)
+    p.seed = int(seed)
+    p.lo_ppm = float(lo_ppm)
+    p.cfo_hz = float(cfo_hz)
+    p.multipath = 1 if multipath else 0
+    p.esn0_db = 1000.0 if esn0_db is None else float(esn0_db)
+    p.differential = 1 if differential else 0
+    dev = torch.device("cuda", device)
+    if out is None:
+        out = torch.empty((n_streams, 2 * n_samples), dtype=torch.float32, device=dev)
+    sps = sample_rate // symbol_rate
+    nsym = (n_samples + 4096) // sps + 2
+    if tx_bits is None:
+        tx_bits = torch.zeros((n_streams, (2 * nsym + 7) // 8 + 8), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    _check(lib().qpsk_synth_generate(C.byref(p), int(device), C.c_void_p(stream or 0), n_streams,
+                                     int(n_samples), out.data_ptr(), out.stride(0),
+                                     tx_bits.data_ptr(), tx_bits.stride(0)))
+    return out, tx_bits

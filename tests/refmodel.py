@@ -264,3 +264,111 @@ class RefDemod:
         rot = [self.costas.process(s[0], s[1]) for s in syms]
         bits, self.diff = decode_bits(rot, self.differential, self.diff)
         return bits, np.array(rot, dtype=F).reshape(-1), y
+
+
+# ---- Band-Edge FLL (Band-Edge Filter.cs:40-202), independent model ----------
+import ctypes as _ct
+
+_libm = _ct.CDLL("libm.so.6")
+_libm.sinf.argtypes = [_ct.c_float]
+_libm.sinf.restype = _ct.c_float
+_libm.cosf.argtypes = [_ct.c_float]
+_libm.cosf.restype = _ct.c_float
+_libm.remainderf.argtypes = [_ct.c_float, _ct.c_float]
+_libm.remainderf.restype = _ct.c_float
+PI_F = F(3.14159274101257324219)
+
+
+def _sinc(x):
+    if x == F(0):
+        return F(1)
+    arg = PI_F * x
+    return F(_libm.sinf(float(arg))) / arg
+
+
+def fll_taps(sps, rolloff, n):
+    sps, rolloff = F(sps), F(rolloff)
+    mid = (n - 1) // 2
+    bb = []
+    s = F(0)
+    for i in range(n):
+        k = F(i - mid) / (F(2) * sps)
+        pos = rolloff * k
+        tap = _sinc(pos - F(0.5)) + _sinc(pos + F(0.5))
+        s = s + tap
+        bb.append(tap)
+    bb = [b / s for b in bb]
+    two_pi = F(2) * PI_F
+    lo, up = [], []
+    for i in range(n):
+        k = F(i - mid) / (F(2) * sps)
+        ang = -two_pi * (F(1) + rolloff) * k
+        wc, ws = F(_libm.cosf(float(ang))), F(_libm.sinf(float(ang)))
+        li, lq = bb[i] * wc, bb[i] * ws
+        lo += [li, lq]
+        up += [li, -lq]
+    return np.array(lo, F), np.array(up, F)
+
+
+class FLL:
+    def __init__(self, sps, rolloff, n, bw, lanes=8):
+        self.lo, self.up = fll_taps(sps, rolloff, n)
+        self.n = n
+        self.lanes = lanes
+        sps = F(sps)
+        self.beta = F(4) * F(bw) / sps
+        self.alpha = F(0)
+        self.maxf = (F(2) * PI_F) * (F(2) / sps)
+        self.phase = F(0)
+        self.freq = F(0)
+        self.hist = [(F(0), F(0))] * n    # last n mixed samples, oldest first
+
+    def _dot(self, taps, win):
+        n, w = self.n, self.lanes
+        hr = [(taps[2 * (n - 1 - k)], taps[2 * (n - 1 - k) + 1]) for k in range(n)]
+        ai = aq = F(0)
+        if w > 1:
+            nvec = n - n % w
+            vi = [F(0)] * w
+            vq = [F(0)] * w
+            for i in range(0, nvec, w):
+                for l in range(w):
+                    (hi, hq), (xi, xq) = hr[i + l], win[i + l]
+                    vi[l] = vi[l] + ((hi * xi) - (hq * xq))
+                    vq[l] = vq[l] + ((hi * xq) + (hq * xi))
+            for l in range(w):
+                ai = ai + vi[l]
+                aq = aq + vq[l]
+            rng = range(nvec, n)
+        else:
+            rng = range(n)
+        for i in rng:
+            (hi, hq), (xi, xq) = hr[i], win[i]
+            ai = ai + ((hi * xi) - (hq * xq))
+            aq = aq + ((hi * xq) + (hq * xi))
+        return ai, aq
+
+    def process(self, x_iq):
+        x = np.asarray(x_iq, F).reshape(-1, 2)
+        out = np.zeros_like(x)
+        two_pi = F(2) * PI_F
+        for t in range(x.shape[0]):
+            s, c = portable_sincos(float(self.phase))
+            s, c = F(s), F(c)
+            xi, xq = x[t, 0], x[t, 1]
+            oi = xi * c - xq * s
+            oq = xi * s + xq * c
+            out[t] = (oi, oq)
+            self.hist = self.hist[1:] + [(oi, oq)]
+            ui, uq = self._dot(self.up, self.hist)
+            li, lq = self._dot(self.lo, self.hist)
+            err = (li * li + lq * lq) - (ui * ui + uq * uq)
+            self.freq = self.freq + self.beta * err
+            self.phase = self.phase + (self.freq + self.alpha * err)
+            if self.phase > two_pi or self.phase < -two_pi:
+                self.phase = F(_libm.remainderf(float(self.phase), float(two_pi)))
+            if self.freq > self.maxf:
+                self.freq = self.maxf
+            elif self.freq < -self.maxf:
+                self.freq = -self.maxf
+        return out.reshape(-1)
