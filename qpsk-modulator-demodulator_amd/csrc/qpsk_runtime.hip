@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -87,8 +88,10 @@ struct qpsk_demod {
     int64_t *d_lengths = nullptr;
     int64_t *h_counts = nullptr;     // pinned
     bool timing = false;
-    hipEvent_t ev[4] = {};
-    float stage_ms[4] = {0, 0, 0, 0};
+    // one set of 5 events per timed call: start, after FLL, after FIR, after
+    // FIR-history, after loop kernel; averaged by qpsk_demod_stage_times()
+    std::vector<std::array<hipEvent_t, 5>> ev_pool;
+    size_t ev_used = 0;
 };
 
 extern "C" {
@@ -176,8 +179,6 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipStreamCreate failed"));
     h->own_stream = true;
-    for (auto &e : h->ev)
-        if (hipEventCreate(&e) != hipSuccess) return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipEventCreate"));
 
     const int64_t S = n_streams;
     h->n_max = p->max_samples_per_call;
@@ -234,8 +235,8 @@ int qpsk_demod_destroy(qpsk_demod *h) {
     hipFree(h->d_counts);
     hipFree(h->d_lengths);
     if (h->h_counts) hipHostFree(h->h_counts);
-    for (auto &e : h->ev)
-        if (e) hipEventDestroy(e);
+    for (auto &set : h->ev_pool)
+        for (auto &e : set) hipEventDestroy(e);
     if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
     delete h;
     return QPSK_OK;
@@ -258,13 +259,24 @@ int qpsk_demod_set_stream(qpsk_demod *h, void *hip_stream) {
 int qpsk_demod_enable_timing(qpsk_demod *h, int32_t on) {
     if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
     h->timing = on != 0;
+    h->ev_used = 0;
     return QPSK_OK;
 }
 
 int qpsk_demod_stage_times(const qpsk_demod *h, float *ms, int32_t n) {
     if (!h || !ms) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    float sum[4] = {0, 0, 0, 0};
+    if (h->ev_used > 0) HIP_TRY(hipEventSynchronize(h->ev_pool[h->ev_used - 1][4]));
+    for (size_t c = 0; c < h->ev_used; ++c) {
+        const auto &e = h->ev_pool[c];
+        float t;
+        HIP_TRY(hipEventElapsedTime(&t, e[0], e[1])); sum[0] += t;
+        HIP_TRY(hipEventElapsedTime(&t, e[1], e[2])); sum[1] += t;
+        HIP_TRY(hipEventElapsedTime(&t, e[3], e[4])); sum[2] += t;
+        HIP_TRY(hipEventElapsedTime(&t, e[0], e[4])); sum[3] += t;
+    }
     const int k = std::min<int32_t>(n, 4);
-    for (int i = 0; i < k; ++i) ms[i] = h->stage_ms[i];
+    for (int i = 0; i < k; ++i) ms[i] = h->ev_used ? sum[i] / h->ev_used : 0.f;
     return k;
 }
 
@@ -305,7 +317,16 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
     }
     hipStream_t st = h->stream;
     HIP_TRY(hipSetDevice(h->p.device));
-    if (h->timing) HIP_TRY(hipEventRecord(h->ev[0], st));
+    hipEvent_t *ev = nullptr;
+    if (h->timing) {
+        if (h->ev_used == h->ev_pool.size()) {
+            std::array<hipEvent_t, 5> set{};
+            for (auto &e : set) HIP_TRY(hipEventCreate(&e));
+            h->ev_pool.push_back(set);
+        }
+        ev = h->ev_pool[h->ev_used++].data();
+        HIP_TRY(hipEventRecord(ev[0], st));
+    }
 
     // ---- input -----------------------------------------------------------
     const float *x = iq;
@@ -337,7 +358,7 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
         x = h->d_fll_out;
         x_stride = h->n_max;
     }
-    if (h->timing) HIP_TRY(hipEventRecord(h->ev[1], st));
+    if (ev) HIP_TRY(hipEventRecord(ev[1], st));
 
     // ---- matched filter (QPSKDeModulator.cs:360) ----------------------------
     FirArgs fa{};
@@ -347,10 +368,12 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
     fa.y = h->d_mf; fa.y_stride = h->mf_stride; fa.y_offset = kMfPrefix;
     if (n_call > 0) {
         launch_fir(fa, h->taps, h->d_hrev, h->T, h->W, S, n_call, st);
+        if (ev) HIP_TRY(hipEventRecord(ev[2], st));
         launch_fir_hist(fa, h->d_hist[h->hist_cur ^ 1], h->T - 1, S, st);
         h->hist_cur ^= 1;
     }
-    if (h->timing) HIP_TRY(hipEventRecord(h->ev[2], st));
+    if (ev && n_call <= 0) HIP_TRY(hipEventRecord(ev[2], st));
+    if (ev) HIP_TRY(hipEventRecord(ev[3], st));
 
     // ---- symbol sync + Costas + decode (QPSKDeModulator.cs:364-408) --------
     LoopArgs la{};
@@ -369,7 +392,7 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
     la.S = S;
     launch_loop(la, h->lp, mode, 64, st);
     HIP_TRY(hipGetLastError());
-    if (h->timing) HIP_TRY(hipEventRecord(h->ev[3], st));
+    if (ev) HIP_TRY(hipEventRecord(ev[4], st));
 
     // ---- outputs -----------------------------------------------------------
     const hipMemcpyKind kind = mem == QPSK_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
@@ -387,13 +410,6 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
     } else {
         if (n_bits) HIP_TRY(hipMemcpyAsync(n_bits, h->d_counts, S * sizeof(int64_t), kind, st));
         if (n_syms) HIP_TRY(hipMemcpyAsync(n_syms, h->d_counts + S, S * sizeof(int64_t), kind, st));
-    }
-    if (h->timing) {
-        HIP_TRY(hipEventSynchronize(h->ev[3]));
-        HIP_TRY(hipEventElapsedTime(&h->stage_ms[0], h->ev[0], h->ev[1]));
-        HIP_TRY(hipEventElapsedTime(&h->stage_ms[1], h->ev[1], h->ev[2]));
-        HIP_TRY(hipEventElapsedTime(&h->stage_ms[2], h->ev[2], h->ev[3]));
-        HIP_TRY(hipEventElapsedTime(&h->stage_ms[3], h->ev[0], h->ev[3]));
     }
     return QPSK_OK;
 }
