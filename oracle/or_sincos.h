@@ -8,7 +8,8 @@
  * CPU test sweeps both and requires bitwise-identical results.
  *
  * Algorithm: Cody-Waite reduction by pi/2 with a three-part constant, then the
- * published fdlibm minimax kernels (__kernel_sin / __kernel_cos, |r| <= pi/4).
+ * published fdlibm minimax coefficients (__kernel_sin / __kernel_cos, |r| <= pi/4),
+ * evaluated in Estrin form.
  * Every operation is an IEEE-754 double op or an explicit fma(), so the result
  * is bit-identical on any IEEE host and on gfx950 (v_fma_f64 is correctly
  * rounded).  Compile with -ffp-contract=off.
@@ -25,48 +26,49 @@ static inline void or_sincos_kernel(double r, double *s, double *c)
     const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
                  C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
                  C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    /* Estrin evaluation (3 fma levels instead of 5): the Costas recurrence
+     * waits on this chain every symbol */
     double z = r * r;
-    /* sin */
-    double ps = fma(z, S6, S5);
-    ps = fma(z, ps, S4);
-    ps = fma(z, ps, S3);
-    ps = fma(z, ps, S2);
-    ps = fma(z, ps, S1);
+    double zz = z * z;
+    /* sin: r + r^3 (S1 + z S2 + z^2 S3 + z^3 S4 + z^4 S5 + z^5 S6) */
+    double sa = fma(z, S2, S1), sb = fma(z, S4, S3), sc = fma(z, S6, S5);
+    double ps = fma(zz, fma(zz, sc, sb), sa);
     double v = z * r;
     *s = fma(v, ps, r);
-    /* cos */
-    double pc = fma(z, C6, C5);
-    pc = fma(z, pc, C4);
-    pc = fma(z, pc, C3);
-    pc = fma(z, pc, C2);
-    pc = fma(z, pc, C1);
+    /* cos: 1 - z/2 + z^2 (C1 + z C2 + ... + z^5 C6), fdlibm tail correction */
+    double ca = fma(z, C2, C1), cb = fma(z, C4, C3), cc = fma(z, C6, C5);
+    double pc = fma(zz, fma(zz, cc, cb), ca);
     double hz = 0.5 * z;
     double w = 1.0 - hz;
-    double zz = z * z;
     *c = w + (((1.0 - w) - hz) + zz * pc);
 }
 
 static inline void or_sincos(double x, double *s, double *c)
 {
+    /* straight-line on the common path (no data-dependent branches besides the
+     * never-taken huge-argument pre-reduction): the GPU Costas loop is
+     * latency-bound and every branch costs an exec-mask round trip */
     const double INVPIO2 = 6.36619772367581382433e-01;
     const double P1 = 1.57079632679489655800e+00;  /* pi/2 rounded to double */
     const double P2 = 6.12323399573676603587e-17;  /* next 53 bits */
     const double P3 = -1.49738490485916983e-33;    /* next bits */
-    if (!(fabs(x) <= 1.0e300)) { *s = x - x; *c = x - x; return; } /* NaN / Inf -> NaN */
-    if (fabs(x) > 1.0e6) x = fmod(x, 6.28318530717958647693);
+    const int bad = !(fabs(x) <= 1.0e300);         /* NaN / Inf -> NaN */
+    if (__builtin_expect(fabs(x) > 1.0e6, 0)) x = bad ? x : fmod(x, 6.28318530717958647693);
     double k = rint(x * INVPIO2);
+    k = bad ? 0.0 : k;
     double r = fma(-k, P1, x);
     r = fma(-k, P2, r);
     r = fma(-k, P3, r);
     double ks, kc;
     or_sincos_kernel(r, &ks, &kc);
-    int q = ((int)k) & 3;
-    switch (q) {
-    case 0: *s = ks; *c = kc; break;
-    case 1: *s = kc; *c = -ks; break;
-    case 2: *s = -ks; *c = -kc; break;
-    default: *s = -kc; *c = ks; break;
-    }
+    const int q = ((int)k) & 3;
+    /* q: 0 -> (s, c), 1 -> (c, -s), 2 -> (-s, -c), 3 -> (-c, s) */
+    double sv = (q & 1) ? kc : ks;
+    double cv = (q & 1) ? ks : kc;
+    sv = (q & 2) ? -sv : sv;
+    cv = ((q + 1) & 2) ? -cv : cv;
+    *s = bad ? x - x : sv;
+    *c = bad ? x - x : cv;
 }
 
 static inline void or_sincosf(float x, float *s, float *c)

@@ -43,6 +43,7 @@ struct LoopArgs {
     int64_t syms_cap;
     int64_t *n_syms;
     int S;
+    unsigned long long *probe;   // diagnostic cycle stamps (QPSK_LOOP_STAMPS builds only)
 };
 
 struct FllArgs {

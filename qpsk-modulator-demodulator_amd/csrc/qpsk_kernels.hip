@@ -198,167 +198,6 @@ __global__ void fir_hist_kernel(FirArgs a, float *hist_new, int H, int S) {
 }
 
 // ---------------------------------------------------------------------------
-// Symbol sync + carrier recovery + decode, one lane per stream
-// ---------------------------------------------------------------------------
-template <int MODE, bool DIFF, bool SYMS>
-__global__ __launch_bounds__(64) void loop_kernel(LoopArgs a, LoopParams P) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.S) return;
-    const int64_t n = a.lengths ? a.lengths[s] : a.n;
-    if (MODE == kModeDemodulate && n == 0) {   // QPSKDeModulator.cs:350-351
-        if (a.n_bits) a.n_bits[s] = 0;
-        if (a.n_syms) a.n_syms[s] = 0;
-        return;
-    }
-    StreamState st = a.state[s];
-    f2 *mf = reinterpret_cast<f2 *>(a.mf) + s * a.mf_stride;
-    const int R = st.carry_n;
-    f2 *buf = mf + kMfPrefix - R;             // logical queue index 0
-    const f2 *carry = reinterpret_cast<const f2 *>(a.carry) + static_cast<int64_t>(s) * kCarryMax;
-    for (int i = 0; i < R; ++i) buf[i] = carry[i];
-    const int64_t count = R + n;              // _bufCount after Append
-    const int64_t cap = n;                    // output span = 2n floats (QPSKDeModulator.cs:366)
-
-    int64_t base = st.base;
-    double mu = st.mu, integ = st.integ;
-    float psi = st.psi, psq = st.psq, pdi = st.pdi, pdq = st.pdq;
-    int has_prev = st.has_prev;
-    double theta = st.theta, freq = st.freq;
-    int diff_have = st.diff_have;
-    float dpi = st.diff_pi, dpq = st.diff_pq;
-    const double sps = P.sps, kp = P.kp, ki = P.ki, ca = P.c_alpha, cb = P.c_beta;
-    const double kTwoPi = 2.0 * 3.14159265358979311600;
-    const double kPi = 3.14159265358979311600;
-
-    uint32_t *bits = a.bits ? a.bits + s * a.bits_stride_words : nullptr;
-    f2 *syms = SYMS ? reinterpret_cast<f2 *>(a.syms) + s * a.syms_stride : nullptr;
-    const int64_t sym_cap = a.syms_cap;
-    uint32_t word = 0;
-    int wbits = 0;
-    int64_t widx = 0, nbits = 0, nsym = 0;
-    int err = st.error;
-
-    while (base + 2 < count) {
-        // CubicLagrange4 (MuellerMuller.cs:160-190), float
-        const f2 xm1 = buf[base - 1], x0 = buf[base], x1 = buf[base + 1], x2 = buf[base + 2];
-        const float t = static_cast<float>(mu);
-        const float tm1 = t - 1.0f, tm2 = t - 2.0f, tp1 = t + 1.0f;
-        const float cm1 = -(t * tm1 * tm2) * (1.0f / 6.0f);
-        const float c0 = (tp1 * tm1 * tm2) * (1.0f / 2.0f);
-        const float c1 = -(tp1 * t * tm2) * (1.0f / 2.0f);
-        const float c2 = (tp1 * t * tm1) * (1.0f / 6.0f);
-        const float ci = cm1 * xm1.x + c0 * x0.x + c1 * x1.x + c2 * x2.x;
-        const float cq = cm1 * xm1.y + c0 * x0.y + c1 * x1.y + c2 * x2.y;
-        const float di = ci >= 0.0f ? 1.0f : -1.0f;
-        const float dq = cq >= 0.0f ? 1.0f : -1.0f;
-        double adv;
-        if (has_prev) {   // M&M TED + PI filter (MuellerMuller.cs:78-91), double
-            const double t1 = static_cast<double>(pdi) * ci + static_cast<double>(pdq) * cq;
-            const double t2 = static_cast<double>(di) * psi + static_cast<double>(dq) * psq;
-            const double e = t1 - t2;
-            integ += ki * e;
-            double corr = kp * e + integ;
-            if (corr > 0.1) corr = 0.1;
-            if (corr < -0.1) corr = -0.1;
-            adv = sps + corr;
-        } else {
-            has_prev = 1;
-            adv = sps;
-        }
-        if (nsym >= cap) break;   // MuellerMuller.cs:101-102 (state kept, no emit)
-
-        // Costas (CostasLoopQpsk.cs:63-92): double NCO, float I/O
-        double sn, cs;
-        qpsk_sincos(theta, &sn, &cs);
-        const double mi = static_cast<double>(ci) * cs + static_cast<double>(cq) * sn;
-        const double mq = static_cast<double>(cq) * cs - static_cast<double>(ci) * sn;
-        const float ri = static_cast<float>(mi), rq = static_cast<float>(mq);
-        const float ei = ri >= 0.0f ? 1.0f : -1.0f;
-        const float eq = rq >= 0.0f ? 1.0f : -1.0f;
-        const double pe = static_cast<double>(ei) * mq - static_cast<double>(eq) * mi;
-        freq += cb * pe;
-        theta += freq + ca * pe;
-        if (theta > kPi) theta -= kTwoPi;
-        else if (theta < -kPi) theta += kTwoPi;
-        if (SYMS) {
-            if (nsym < sym_cap) syms[nsym] = f2{ri, rq};
-            else err |= 2;
-        }
-        if (MODE == kModeDemodulate) {
-            // Decision + differential decode (QPSKDeModulator.cs:379-407)
-            bool emit = true;
-            uint32_t b2 = 0;
-            if (DIFF) {
-                if (!diff_have) {
-                    dpi = ei; dpq = eq;
-                    diff_have = 1;
-                    emit = false;
-                } else {
-                    const float del_i = ei * dpi + eq * dpq;
-                    const float del_q = eq * dpi - ei * dpq;
-                    dpi = ei; dpq = eq;
-                    if (fabsf(del_i) >= fabsf(del_q)) b2 = del_i >= 0.0f ? 0u : 3u;  // 00 / 11
-                    else b2 = del_q >= 0.0f ? 1u : 2u;                               // 01 / 10
-                }
-            } else {
-                b2 = (ei < 0.0f ? 0u : 2u) | (eq < 0.0f ? 0u : 1u);                  // :304-318
-            }
-            if (emit) {
-                word = (word << 2) | b2;
-                wbits += 2;
-                nbits += 2;
-                if (wbits == 32) {
-                    if (widx < a.bits_cap_words) bits[widx] = __builtin_bswap32(word);
-                    else err |= 2;
-                    ++widx;
-                    word = 0;
-                    wbits = 0;
-                }
-            }
-        }
-        ++nsym;
-        psi = ci; psq = cq;
-        pdi = di; pdq = dq;
-        const double nt = static_cast<double>(base) + mu + adv;   // MuellerMuller.cs:113
-        const double fl = floor(nt);
-        base = static_cast<int64_t>(fl);
-        mu = nt - fl;
-        if (base + 1 >= count) break;
-    }
-    if (MODE == kModeDemodulate && wbits > 0) {
-        if (widx < a.bits_cap_words) bits[widx] = __builtin_bswap32(word << (32 - wbits));
-        else err |= 2;
-    }
-    // Drop consumed samples, keep the rest for the next call (MuellerMuller.cs:123-133)
-    int64_t consumed = base - 1 > 0 ? base - 1 : 0;
-    const int64_t keep_min = count - 3 > 0 ? count - 3 : 0;
-    if (keep_min < consumed) consumed = keep_min;
-    int64_t keep = count - consumed;
-    if (keep > kCarryMax) {
-        err |= 1;
-        consumed = count - kCarryMax;
-        keep = kCarryMax;
-    }
-    f2 *carry_w = reinterpret_cast<f2 *>(a.carry) + static_cast<int64_t>(s) * kCarryMax;
-    for (int64_t i = 0; i < keep; ++i) carry_w[i] = buf[consumed + i];
-    st.base = static_cast<int32_t>(base - consumed);
-    st.carry_n = static_cast<int32_t>(keep);
-    st.mu = mu; st.integ = integ;
-    st.psi = psi; st.psq = psq; st.pdi = pdi; st.pdq = pdq;
-    st.has_prev = has_prev;
-    st.theta = theta; st.freq = freq;
-    if (MODE == kModeDemodulate) {
-        st.diff_have = diff_have;
-        st.diff_pi = dpi;
-        st.diff_pq = dpq;
-    }
-    st.error = err;
-    a.state[s] = st;
-    if (a.n_bits) a.n_bits[s] = MODE == kModeDemodulate ? nbits : 0;
-    if (a.n_syms) a.n_syms[s] = nsym;
-}
-
-// ---------------------------------------------------------------------------
 // Band-Edge FLL, one lane per stream (exact reference order)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void fll_dot(const float *taps_rev, const f2 *win, int W, float *oi,
@@ -492,27 +331,6 @@ void launch_fir_hist(const FirArgs &a, float *hist_new, int H, int S, hipStream_
                        dim3(threads), 0, stream, a, hist_new, H, S);
 }
 
-void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int lanes_per_block,
-                 hipStream_t stream) {
-    const int threads = lanes_per_block > 0 ? lanes_per_block : 64;
-    dim3 grid((a.S + threads - 1) / threads);
-    const bool syms = a.syms != nullptr;
-    const bool diff = P.differential != 0;
-    if (mode == kModeConstellation) {
-        hipLaunchKernelGGL((loop_kernel<kModeConstellation, false, true>), grid, dim3(threads), 0,
-                           stream, a, P);
-    } else if (diff) {
-        if (syms)
-            hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, true>), grid, dim3(threads), 0, stream, a, P);
-        else
-            hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, false>), grid, dim3(threads), 0, stream, a, P);
-    } else {
-        if (syms)
-            hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, true>), grid, dim3(threads), 0, stream, a, P);
-        else
-            hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, false>), grid, dim3(threads), 0, stream, a, P);
-    }
-}
 
 void launch_fll(const FllArgs &a, const FllParams &P, hipStream_t stream) {
     const int threads = 64;

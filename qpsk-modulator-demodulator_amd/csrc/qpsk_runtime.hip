@@ -182,7 +182,7 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
 
     const int64_t S = n_streams;
     h->n_max = p->max_samples_per_call;
-    h->mf_stride = ((kMfPrefix + h->n_max + 63) / 64) * 64;
+    h->mf_stride = ((kMfPrefix + h->n_max + 2 + 63) / 64) * 64;   // + row slack for the loop loader
     h->syms_cap = qpsk_demod_max_symbols(h, h->n_max);
     h->bits_words = (2 * h->syms_cap + 31) / 32 + 1;
     const int H = h->T - 1;
@@ -390,7 +390,7 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
     la.syms_cap = h->syms_cap;
     la.n_syms = h->d_counts + S;
     la.S = S;
-    launch_loop(la, h->lp, mode, 64, st);
+    launch_loop(la, h->lp, mode, 0, st);
     HIP_TRY(hipGetLastError());
     if (ev) HIP_TRY(hipEventRecord(ev[4], st));
 

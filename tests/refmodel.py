@@ -166,17 +166,16 @@ def portable_sincos(x):
     r = _fma(-k, 6.12323399573676603587e-17, r)
     r = _fma(-k, -1.49738490485916983e-33, r)
     z = r * r
-    ps = _fma(z, _S[5], _S[4])
-    for c in (_S[3], _S[2], _S[1], _S[0]):
-        ps = _fma(z, ps, c)
+    zz = z * z
+    sa, sb, sc = _fma(z, _S[1], _S[0]), _fma(z, _S[3], _S[2]), _fma(z, _S[5], _S[4])
+    ps = _fma(zz, _fma(zz, sc, sb), sa)
     v = z * r
     ks = _fma(v, ps, r)
-    pc = _fma(z, _C[5], _C[4])
-    for c in (_C[3], _C[2], _C[1], _C[0]):
-        pc = _fma(z, pc, c)
+    ca, cb, cc = _fma(z, _C[1], _C[0]), _fma(z, _C[3], _C[2]), _fma(z, _C[5], _C[4])
+    pc = _fma(zz, _fma(zz, cc, cb), ca)
     hz = 0.5 * z
     w = 1.0 - hz
-    kc = w + (((1.0 - w) - hz) + (z * z) * pc)
+    kc = w + (((1.0 - w) - hz) + zz * pc)
     q = int(k) & 3
     return [(ks, kc), (kc, -ks), (-ks, -kc), (-kc, ks)][q]
 
