@@ -51,30 +51,34 @@ QPSK_HD static inline void qpsk_sincos_kernel(double r, double *s, double *c)
 
 QPSK_HD static inline void qpsk_sincos(double x, double *s, double *c)
 {
-    /* straight-line on the common path (no data-dependent branches besides the
-     * never-taken huge-argument pre-reduction): the GPU Costas loop is
-     * latency-bound and every branch costs an exec-mask round trip */
+    /* straight-line on the common path: the GPU Costas loop is issue-bound and
+     * every branch or select costs issue slots.  NaN propagates through the
+     * arithmetic; |x| > 1e6 (and +-Inf -> NaN) take a pre-reduction branch
+     * that the Costas loop never reaches (theta is wrapped to [-pi, pi]). */
     const double INVPIO2 = 6.36619772367581382433e-01;
     const double P1 = 1.57079632679489655800e+00;  /* pi/2 rounded to double */
     const double P2 = 6.12323399573676603587e-17;  /* next 53 bits */
     const double P3 = -1.49738490485916983e-33;    /* next bits */
-    const int bad = !(fabs(x) <= 1.0e300);         /* NaN / Inf -> NaN */
-    if (__builtin_expect(fabs(x) > 1.0e6, 0)) x = bad ? x : fmod(x, 6.28318530717958647693);
-    double k = rint(x * INVPIO2);
-    k = bad ? 0.0 : k;
+    if (__builtin_expect(fabs(x) > 1.0e6, 0)) x = fmod(x, 6.28318530717958647693);
+    const double k = rint(x * INVPIO2);
     double r = fma(-k, P1, x);
     r = fma(-k, P2, r);
     r = fma(-k, P3, r);
     double ks, kc;
     qpsk_sincos_kernel(r, &ks, &kc);
-    const int q = ((int)k) & 3;
+    /* quadrant = low bits of the integer k (|k| < 2^20): k + 1.5*2^52 puts
+     * them in the low mantissa bits; well defined for NaN too (result is NaN) */
+    union { double d; unsigned long long u; } kb;
+    kb.d = k + 6755399441055744.0;
+    const unsigned q = (unsigned)(kb.u & 3u);
     /* q: 0 -> (s, c), 1 -> (c, -s), 2 -> (-s, -c), 3 -> (-c, s) */
-    double sv = (q & 1) ? kc : ks;
-    double cv = (q & 1) ? ks : kc;
-    sv = (q & 2) ? -sv : sv;
-    cv = ((q + 1) & 2) ? -cv : cv;
-    *s = bad ? x - x : sv;
-    *c = bad ? x - x : cv;
+    union { double d; unsigned long long u; } sv, cv;
+    sv.d = (q & 1u) ? kc : ks;
+    cv.d = (q & 1u) ? ks : kc;
+    sv.u ^= (unsigned long long)(q & 2u) << 62;
+    cv.u ^= (unsigned long long)((q + 1u) & 2u) << 62;
+    *s = sv.d;
+    *c = cv.d;
 }
 
 QPSK_HD static inline void qpsk_sincosf(float x, float *s, float *c)

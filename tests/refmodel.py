@@ -157,9 +157,9 @@ _C = [4.16666666666666019037e-02, -1.38888888888741095749e-03, 2.480158728947672
 
 
 def portable_sincos(x):
-    if not (abs(x) <= 1.0e300):
-        return math.nan, math.nan
-    if abs(x) > 1.0e6:
+    if not (abs(x) <= 1.0e6):   # huge, +-Inf (-> NaN) and NaN
+        if math.isnan(x) or math.isinf(x):
+            return math.nan, math.nan
         x = math.fmod(x, 6.28318530717958647693)
     k = float(round(x * 6.36619772367581382433e-01))  # rint: half-even
     r = _fma(-k, 1.57079632679489655800e+00, x)

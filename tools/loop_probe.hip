@@ -36,9 +36,9 @@ int main(int argc, char** argv) {
   printf("S=%d n=%lld spw=%d: %.3f ms, stream0 symbols %lld -> %.1f ns/symbol\n", S, (long long)n, spw, ms, (long long)ns, ms * 1e6 / ns);
   for (int b = 0; b < 3; ++b) {
     auto* p = &pr[8 * b];
-    printf(" WG %d: loader wait %.0f bar %.0f issue %.0f | consumer bar %.0f loop %.0f iters %llu rounds %llu  (cycles/round: lw %.0f lb %.0f li %.0f cb %.0f cl %.0f; cyc/iter %.0f)\n",
-           b, (double)p[0], (double)p[1], (double)p[2], (double)p[3], (double)p[4], p[5], p[6],
-           (double)p[0] / p[6], (double)p[1] / p[6], (double)p[2] / p[6], (double)p[3] / p[6], (double)p[4] / p[6], (double)p[4] / p[5]);
+    const double R = (double)p[7];
+    printf(" WG %d rounds %llu: per round cycles: loader wait %.0f bar %.0f | M&M bar %.0f loop %.0f | Costas bar %.0f loop %.0f | M&M cyc/sym %.0f\n",
+           b, p[7], p[0] / R, p[1] / R, p[2] / R, p[3] / R, p[5] / R, p[6] / R, (double)p[3] / p[4]);
   }
   return 0;
 }
