@@ -170,7 +170,9 @@ typedef struct qpsk_synth_params {
     double cfo_hz;
     int32_t multipath;
     double esn0_db;
-    int32_t reserved[8];
+    int64_t first_stream;       /* global id of row 0: a rank's shard draws the same
+                                   streams whatever the sharding */
+    int32_t reserved[6];
 } qpsk_synth_params;
 void qpsk_synth_params_init(qpsk_synth_params *p, int32_t sample_rate, int32_t symbol_rate);
 int qpsk_synth_generate(const qpsk_synth_params *p, int32_t device, void *hip_stream,

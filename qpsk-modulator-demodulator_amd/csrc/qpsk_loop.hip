@@ -477,9 +477,10 @@ static void launch_loop_spw(const LoopArgs &a, const LoopParams &P, int mode, hi
 void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int streams_per_block,
                  hipStream_t stream) {
     hipLaunchKernelGGL(carry_prefix_kernel, dim3(a.S), dim3(64), 0, stream, a);
-    // the loop is latency-bound per stream: fewer streams per workgroup spread
-    // the batch over more CUs (each with its own LDS / issue ports)
-    if (streams_per_block == 16 || (streams_per_block <= 0 && a.S <= 2048))
+    // the loop is latency-bound per stream and a wave's lanes are free, so
+    // 32 streams per workgroup; measured faster than 16 even at S=256, where
+    // only 8 CUs are busy (profiles/r01_loop_probe.txt)
+    if (streams_per_block == 16)
         launch_loop_spw<16>(a, P, mode, stream);
     else
         launch_loop_spw<32>(a, P, mode, stream);

@@ -45,6 +45,7 @@ struct SynthArgs {
     int mid;              // (T-1)/2
     int G;                // composite pulse length (T + multipath taps - 1)
     uint64_t seed;
+    int64_t s0;           // global id of row 0 (qpsk_synth_params.first_stream)
     double cfo_hz, lo_ppm, lo_hz, fs;
     double noise_sigma;   // per component, 0 = none
     int differential;
@@ -63,7 +64,8 @@ struct Pulse {
 __global__ void synth_symbols_kernel(SynthArgs a) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= a.S) return;
-    uint64_t rng = a.seed ^ (0x5159534BULL + static_cast<uint64_t>(s) * 0x9E3779B97F4A7C15ULL);
+    const uint64_t gs = static_cast<uint64_t>(a.s0 + s);
+    uint64_t rng = a.seed ^ (0x5159534BULL + gs * 0x9E3779B97F4A7C15ULL);
     uint8_t *q = a.quad + s * a.nsym;
     uint8_t *b = a.bits ? a.bits + s * a.bits_stride : nullptr;
     // quadrant k <-> (cos, sin)(pi/4 + k pi/2); reference (1/sqrt2)(1+j) = 0
@@ -114,7 +116,8 @@ __global__ void synth_samples_kernel(SynthArgs a, Pulse p) {
         yi += p.re[k] * qim[qq] + p.im[k] * qre[qq];
     }
     // per-stream carrier: +-ppm LO pair (testAtDataLevel.cs:27-28) or +-cfo_hz
-    uint64_t rs = a.seed ^ (0xC0FFEE123ULL + static_cast<uint64_t>(s) * 0xD1B54A32D192ED03ULL);
+    const uint64_t gs = static_cast<uint64_t>(a.s0 + s);
+    uint64_t rs = a.seed ^ (0xC0FFEE123ULL + gs * 0xD1B54A32D192ED03ULL);
     const double u1 = u01(splitmix64(rs)), u2 = u01(splitmix64(rs)), u3 = u01(splitmix64(rs));
     double f = 0.0;
     if (a.cfo_hz > 0.0) f = (2.0 * u1 - 1.0) * a.cfo_hz;
@@ -125,7 +128,7 @@ __global__ void synth_samples_kernel(SynthArgs a, Pulse p) {
     double zr = yr * cs - yi * sn;
     double zi = yr * sn + yi * cs;
     if (a.noise_sigma > 0.0) {
-        uint64_t h = a.seed ^ (static_cast<uint64_t>(s) << 40) ^ static_cast<uint64_t>(i) ^ 0xA5A5A5A5ULL;
+        uint64_t h = a.seed ^ (gs << 40) ^ static_cast<uint64_t>(i) ^ 0xA5A5A5A5ULL;
         const double n1 = 1.0 - u01(splitmix64(h));
         const double n2 = 1.0 - u01(splitmix64(h));
         const double mag = sqrt(-2.0 * log(n1)) * a.noise_sigma;
@@ -195,6 +198,7 @@ int qpsk_synth_generate(const qpsk_synth_params *p, int32_t device, void *hip_st
     a.G = G;
     a.nsym = (n_samples + a.mid) / sps + 2;
     a.seed = p->seed;
+    a.s0 = p->first_stream;
     a.cfo_hz = p->cfo_hz;
     a.lo_ppm = p->lo_ppm;
     a.lo_hz = 100e6;

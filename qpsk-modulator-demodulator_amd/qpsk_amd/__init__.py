@@ -72,7 +72,8 @@ class SynthParams(C.Structure):
         ("cfo_hz", C.c_double),
         ("multipath", C.c_int32),
         ("esn0_db", C.c_double),
-        ("reserved", C.c_int32 * 8),
+        ("first_stream", C.c_int64),
+        ("reserved", C.c_int32 * 6),
     ]
 
 
@@ -427,7 +428,8 @@ class QPSKDeModulator:
 
 def synth_generate(n_streams, n_samples, sample_rate, symbol_rate, rrc_alpha=float(np.float32(0.4)),
                    rrc_span=8, seed=0x5159534B, lo_ppm=1.0, cfo_hz=0.0, multipath=False,
-                   esn0_db=None, differential=True, device=0, stream=None, out=None, tx_bits=None):
+                   esn0_db=None, differential=True, device=0, stream=None, out=None, tx_bits=None,
+                   first_stream=0):
     """Batched synthetic baseband straight into HBM (torch tensors)."""
     import torch
     p = SynthParams()
@@ -440,6 +442,7 @@ def synth_generate(n_streams, n_samples, sample_rate, symbol_rate, rrc_alpha=flo
     p.multipath = 1 if multipath else 0
     p.esn0_db = 1000.0 if esn0_db is None else float(esn0_db)
     p.differential = 1 if differential else 0
+    p.first_stream = int(first_stream)
     dev = torch.device("cuda", device)
     if out is None:
         out = torch.empty((n_streams, 2 * n_samples), dtype=torch.float32, device=dev)
