@@ -62,7 +62,10 @@ typedef struct qpsk_demod_params {
                                        reproduces: 8 (x64 AVX2, default), 4 (ARM64), 1 (no SIMD) */
     int32_t device;                 /* HIP device ordinal                               */
     int64_t max_samples_per_call;   /* complex samples per stream per call (device buffers) */
-    int32_t reserved[8];
+    int32_t loop_variant;           /* symbol-loop kernel shape: 0 = auto,
+                                       1 = 16 streams x 64-sample rounds, 2 = 32 x 64,
+                                       3 = 16 x 128 (sps >= 2 only); results are identical */
+    int32_t reserved[7];
 } qpsk_demod_params;
 
 typedef struct qpsk_demod qpsk_demod;

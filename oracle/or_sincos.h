@@ -7,9 +7,11 @@
  * published algorithm (qpsk-modulator-demodulator_amd/csrc/qpsk_sincos.h); a
  * CPU test sweeps both and requires bitwise-identical results.
  *
- * Algorithm: Cody-Waite reduction by pi/2 with a three-part constant, then the
- * published fdlibm minimax coefficients (__kernel_sin / __kernel_cos, |r| <= pi/4),
- * evaluated in Estrin form.
+ * Algorithm: Cody-Waite reduction by pi/256 with a three-part constant
+ * (fma), a 512-entry table of correctly rounded sin/cos(k pi/256)
+ * (tools/gen_sincos_table.py), degree-5/6 Taylor polynomials for the residual
+ * |r| <= pi/512 and angle addition with the table value added last.
+ * Accuracy <= 1 ulp (table rounding + one final rounding).
  * Every operation is an IEEE-754 double op or an explicit fma(), so the result
  * is bit-identical on any IEEE host and on gfx950 (v_fma_f64 is correctly
  * rounded).  Compile with -ffp-contract=off.
@@ -17,69 +19,80 @@
 #ifndef OR_SINCOS_H
 #define OR_SINCOS_H
 #include <math.h>
+#include "or_sincos_table.h"
 
-static inline void or_sincos_kernel(double r, double *s, double *c)
+/* [2k] = sin(k pi/256), [2k+1] = cos(k pi/256), k < 512: correctly rounded
+ * double + float tail (tools/gen_sincos_table.py) */
+static const double or_sincos_table[1024] = { OR_SINCOS_TAB_VALUES_HI };
+static const double or_sincos_table_lo[1024] = { OR_SINCOS_TAB_VALUES_LO };
+
+/* argument the table reduction accepts: |x| <= 1e6 (or NaN).  Larger |x| and
+ * +-Inf are pre-reduced with fmod (Inf -> NaN); the Costas loop, whose theta
+ * is wrapped to about [-pi, pi], applies this only after a wrap. */
+static inline double or_sincos_arg(double x)
 {
-    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
-    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
-    /* Estrin evaluation (3 fma levels instead of 5): the Costas recurrence
-     * waits on this chain every symbol */
-    double z = r * r;
-    double zz = z * z;
-    /* sin: r + r^3 (S1 + z S2 + z^2 S3 + z^3 S4 + z^4 S5 + z^5 S6) */
-    double sa = fma(z, S2, S1), sb = fma(z, S4, S3), sc = fma(z, S6, S5);
-    double ps = fma(zz, fma(zz, sc, sb), sa);
-    double v = z * r;
-    *s = fma(v, ps, r);
-    /* cos: 1 - z/2 + z^2 (C1 + z C2 + ... + z^5 C6), fdlibm tail correction */
-    double ca = fma(z, C2, C1), cb = fma(z, C4, C3), cc = fma(z, C6, C5);
-    double pc = fma(zz, fma(zz, cc, cb), ca);
-    double hz = 0.5 * z;
-    double w = 1.0 - hz;
-    *c = w + (((1.0 - w) - hz) + zz * pc);
+    return fabs(x) > 1.0e6 ? fmod(x, 6.28318530717958647693) : x;
+}
+
+/* sin and cos of x, |x| <= 1e6 or NaN, given the 512-entry table (any address
+ * space: the GPU kernels pass a copy staged in LDS).  Straight-line: the GPU
+ * Costas loop is issue-bound and every instruction costs issue slots.  NaN
+ * propagates (any table index gives NaN). */
+static inline void or_sincos_tab_core(double x, const double *tab, const double *lo,
+                                           double *s, double *c)
+{
+    const double INV = 0x1.45f306dc9c883p+6;      /* 256/pi */
+    const double P1 = 0x1.921fb54442d18p-7;       /* pi/256 rounded to double */
+    const double P2 = 0x1.1a62633145c07p-61;      /* next 53 bits */
+    const double P3 = -0x1.f1976b7ed8fbcp-117;    /* next bits */
+    const double S3 = -0x1.5555555555555p-3, S5 = 0x1.1111111111111p-7;    /* -1/6, 1/120 */
+    const double C4 = 0x1.5555555555555p-5, C6 = -0x1.6c16c16c16c17p-10;  /* 1/24, -1/720 */
+    const double k = rint(x * INV);
+    double r = fma(-k, P1, x);                    /* Cody-Waite: |r| <= pi/512 */
+    r = fma(-k, P2, r);
+    r = fma(-k, P3, r);
+    /* table index = k mod 512: k + 1.5*2^52 puts the two's-complement low bits
+     * of the integer k in the low mantissa bits (|k| < 2^27 here) */
+    union { double d; unsigned long long u; } kb;
+    kb.d = k + 6755399441055744.0;
+    const unsigned i = (unsigned)(kb.u & 511u);
+    const double ts = tab[2 * i], tc = tab[2 * i + 1];
+    const double ls = lo[2 * i], lc = lo[2 * i + 1];
+    /* sin r = r + r^3(-1/6 + r^2/120), cos r - 1 = r^2(-1/2 + r^2/24 - r^4/720):
+     * truncation < 1e-19 relative for |r| <= pi/512 */
+    const double z = r * r;
+    const double r3p = (r * z) * fma(z, S5, S3);          /* sin r - r */
+    const double cm = z * fma(z, fma(z, C6, C4), -0.5);   /* cos r - 1 */
+    /* angle addition, small terms first: sin x = ts + [tc r + (tc r3p + ts cm + ls)],
+     * one significant rounding in the bracket and one in the final add: <= 1 ulp */
+    *s = ts + fma(tc, r, fma(tc, r3p, fma(ts, cm, ls)));
+    *c = tc + fma(-ts, r, fma(-ts, r3p, fma(tc, cm, lc)));
+}
+
+/* any x: the pre-reduction branch, then the table reduction */
+static inline void or_sincos_tab(double x, const double *tab, const double *lo, double *s,
+                                      double *c)
+{
+    if (__builtin_expect(fabs(x) > 1.0e6, 0)) x = or_sincos_arg(x);
+    or_sincos_tab_core(x, tab, lo, s, c);
 }
 
 static inline void or_sincos(double x, double *s, double *c)
 {
-    /* straight-line on the common path: the GPU Costas loop is issue-bound and
-     * every branch or select costs issue slots.  NaN propagates through the
-     * arithmetic; |x| > 1e6 (and +-Inf -> NaN) take a pre-reduction branch
-     * that the Costas loop never reaches (theta is wrapped to [-pi, pi]). */
-    const double INVPIO2 = 6.36619772367581382433e-01;
-    const double P1 = 1.57079632679489655800e+00;  /* pi/2 rounded to double */
-    const double P2 = 6.12323399573676603587e-17;  /* next 53 bits */
-    const double P3 = -1.49738490485916983e-33;    /* next bits */
-    if (__builtin_expect(fabs(x) > 1.0e6, 0)) x = fmod(x, 6.28318530717958647693);
-    const double k = rint(x * INVPIO2);
-    double r = fma(-k, P1, x);
-    r = fma(-k, P2, r);
-    r = fma(-k, P3, r);
-    double ks, kc;
-    or_sincos_kernel(r, &ks, &kc);
-    /* quadrant = low bits of the integer k (|k| < 2^20): k + 1.5*2^52 puts
-     * them in the low mantissa bits; well defined for NaN too (result is NaN) */
-    union { double d; unsigned long long u; } kb;
-    kb.d = k + 6755399441055744.0;
-    const unsigned q = (unsigned)(kb.u & 3u);
-    /* q: 0 -> (s, c), 1 -> (c, -s), 2 -> (-s, -c), 3 -> (-c, s) */
-    union { double d; unsigned long long u; } sv, cv;
-    sv.d = (q & 1u) ? kc : ks;
-    cv.d = (q & 1u) ? ks : kc;
-    sv.u ^= (unsigned long long)(q & 2u) << 62;
-    cv.u ^= (unsigned long long)((q + 1u) & 2u) << 62;
-    *s = sv.d;
-    *c = cv.d;
+    or_sincos_tab(x, or_sincos_table, or_sincos_table_lo, s, c);
+}
+
+static inline void or_sincosf_tab(float x, const double *tab, const double *lo, float *s,
+                                       float *c)
+{
+    double sd, cd;
+    or_sincos_tab((double)x, tab, lo, &sd, &cd);
+    *s = (float)sd;
+    *c = (float)cd;
 }
 
 static inline void or_sincosf(float x, float *s, float *c)
 {
-    double sd, cd;
-    or_sincos((double)x, &sd, &cd);
-    *s = (float)sd;
-    *c = (float)cd;
+    or_sincosf_tab(x, or_sincos_table, or_sincos_table_lo, s, c);
 }
 #endif

@@ -62,7 +62,7 @@ struct FllArgs {
 bool launch_fir(const FirArgs &a, const TapsRev &taps, const float *hrev_dev, int T, int W, int S,
                 int64_t n_max, hipStream_t stream);
 void launch_fir_hist(const FirArgs &a, float *hist_new, int H, int S, hipStream_t stream);
-void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int lanes_per_block,
+void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant,
                  hipStream_t stream);
 void launch_fll(const FllArgs &a, const FllParams &P, hipStream_t stream);
 

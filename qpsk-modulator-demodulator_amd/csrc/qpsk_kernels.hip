@@ -236,6 +236,13 @@ __device__ __forceinline__ void fll_dot(const float *taps_rev, const f2 *win, in
 }
 
 __global__ __launch_bounds__(64) void fll_kernel(FllArgs a, FllParams P) {
+    __shared__ double tab[1024];
+    __shared__ double tab_lo[1024];
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+        tab[i] = qpsk_sincos_table_dev[i];
+        tab_lo[i] = qpsk_sincos_table_dev_lo[i];
+    }
+    __syncthreads();
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= a.S) return;
     const int64_t n = a.lengths ? a.lengths[s] : a.n;
@@ -253,7 +260,7 @@ __global__ __launch_bounds__(64) void fll_kernel(FllArgs a, FllParams P) {
     for (int64_t t = 0; t < n; ++t) {
         const f2 in = x[t];
         float sn, cs;
-        qpsk_sincosf(phase, &sn, &cs);
+        qpsk_sincosf_tab(phase, tab, tab_lo, &sn, &cs);
         const float oi = in.x * cs - in.y * sn;
         const float oq = in.x * sn + in.y * cs;
         y[t] = f2{oi, oq};

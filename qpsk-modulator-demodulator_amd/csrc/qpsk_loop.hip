@@ -50,12 +50,20 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 #define ACC(acc, t0)
 #endif
 
-constexpr int kB = 64;            // samples per round per stream
-constexpr int kRing = 4 * kB;     // per-stream sample ring (4 rounds): index = p & (kRing-1)
-constexpr int kMir = 4;           // mirror of the ring's last samples in front of it, so the
-                                  // 4 interpolation taps are always contiguous in LDS
-constexpr int kRowS = kMir + kRing;   // per-stream LDS row: [mirror 4][ring 256]
-constexpr int kSymCap = 80;       // symbols per round per stream: <= 67 / (sps - 0.1) + 1, sps >= 1
+// KB = samples per round per stream (template: 64 or 128).  The per-stream
+// sample ring holds 4 rounds (index = p & (4*KB - 1)), preceded by a mirror of
+// its last 4 samples so the 4 interpolation taps are always contiguous in LDS.
+constexpr int kMir = 4;
+template <int KB> struct Ring {
+    static constexpr int len = 4 * KB;
+    static constexpr int row = kMir + len;   // per-stream LDS row: [mirror 4][ring]
+};
+// symbols per round per stream (template CAP): at most floor((KB + 3) / (sps - 0.1)) + 1
+// start in one round: 75 (KB 64, sps >= 1), 36 (KB 64, sps >= 2), 69 (KB 128, sps >= 2)
+constexpr int kCapAny = 80;
+constexpr int kCapSps2 = 40;
+constexpr int kCap128Sps2 = 72;
+typedef double d2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int wave_max_i32(int v) {
 #pragma unroll
@@ -82,19 +90,30 @@ __global__ void carry_prefix_kernel(LoopArgs a) {
     for (int i = threadIdx.x; i < R; i += blockDim.x) mf[i] = c[i];
 }
 
-template <int SPW>
+// Symbol rows are CAP + 1 entries long: an odd stride puts the 32 streams'
+// entry k (read by all lanes at once in the Costas loop) on distinct banks;
+// a stride of 40 made them 16- to 32-way bank conflicts.
+template <int CAP>
+struct RowStride { static constexpr int value = CAP + 1; };
+
+template <int SPW, int CAP, int KB>
 struct LoopLds {
-    f2 mf[SPW * kRowS];            // sample ring   [stream][mirror | 4 rounds x kB]
-    f2 sym[2 * SPW * kSymCap];     // M&M -> Costas [slot][stream][kSymCap]
-    f2 rot[2 * SPW * kSymCap];     // Costas -> decode
-    int cnt[4 * SPW];              // symbols produced by the M&M in round r: cnt[r & 3]
+    static constexpr int RS = RowStride<CAP>::value;
+    f2 mf[SPW * Ring<KB>::row];    // sample ring   [stream][mirror | 4 rounds x KB]
+    d2 sym[2 * SPW * RS];          // M&M -> Costas [slot][stream][RS], widened to double
+    f2 rot[2 * SPW * RS];          // Costas -> decode
+    double tab[1024];              // sincos table head (qpsk_sincos.h)
+    double tab_lo[1024];           // sincos table tail (float values, widened)
+    int cnt[4 * SPW + 4];          // symbols produced by the M&M in round r: cnt[r & 3];
+                                   // cnt[4*SPW + (r & 3)] = their minimum over the batch
 };
 
-template <int MODE, bool DIFF, bool SYMS, int SPW>
+template <int MODE, bool DIFF, bool SYMS, int SPW, int CAP, int KB>
 __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
+    constexpr int kRing = Ring<KB>::len, kRowS = Ring<KB>::row;
     // one LDS object only: a second __shared__ object would make hipcc drain the
     // loader's LDS-DMA before touching it (cdna_hip_programming.md §5)
-    __shared__ LoopLds<SPW> L;
+    __shared__ LoopLds<SPW, CAP, KB> L;
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -111,23 +130,29 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         // DeModulate with an empty span returns before touching any state (:350-351)
         if (MODE == kModeDemodulate && n == 0) cnt = 0;
     }
-    const int NR = (wave_max_i32(cnt) + kB - 1) / kB;
+    const int NR = (wave_max_i32(cnt) + KB - 1) / KB;
     const bool mine = valid && cnt > 0;
+
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+        L.tab[i] = qpsk_sincos_table_dev[i];
+        L.tab_lo[i] = qpsk_sincos_table_dev_lo[i];
+    }
+    __syncthreads();
 
     if (wave == 0) {
         // ============================================================ loader
-        // one glds instruction = 32 lanes x 16 B = one stream's round (512 B)
+        // one glds instruction = KB/2 lanes x 16 B = one stream's round (8*KB bytes)
         const int64_t org = valid ? s * a.mf_stride + kMfPrefix - R - d : 0;
-        const int c2 = 2 * (lane & 31);
+        const int c2 = 2 * (lane % (KB / 2));
         const f2 *mf = reinterpret_cast<const f2 *>(a.mf);
-        const bool lo_half = lane < 32;
+        const bool lo_half = lane < KB / 2;
         auto issue = [&](int r) {
-            const int roff = (r & 3) * kB;
+            const int roff = (r & 3) * KB;
 #pragma unroll 4
             for (int j = 0; j < SPW; ++j) {
                 const int c = __builtin_amdgcn_readlane(cnt, j);
                 const int64_t o = readlane64(org, j);
-                int p = r * kB + c2;
+                int p = r * KB + c2;
                 // past the stream's end: read a harmless in-row pair (never used);
                 // a pair straddling the end reads one sample of row slack
                 if (p >= c) p = 0;
@@ -169,15 +194,24 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         float psi = st.psi, psq = st.psq, pdi = st.pdi, pdq = st.pdq;
         int has_prev = mine ? st.has_prev : 1;
         const double sps = P.sps, kp = P.kp, ki = P.ki;
-        const double dd = static_cast<double>(d);
         const int cap = n;                          // output span = 2n floats (QPSKDeModulator.cs:366)
+        const int kfull = static_cast<int>(floor(static_cast<double>(KB) / (sps + 0.1)));
         int nsym = 0;
         bool stop = !mine;                          // capacity reached (MuellerMuller.cs:101-102)
         f2 *row = L.mf + lane * kRowS;
         // taps x[b-1..b+2] of physical index b: contiguous thanks to the mirror
         auto taps = [&](int b) -> const f2 * { return row + kMir - 3 + ((b + 2) & (kRing - 1)); };
-        // the TED reuses the previous symbol widened to double (MuellerMuller.cs:78-80)
+        // logical time baseIndex + mu.  After baseIndex = floor(t), mu = t - baseIndex
+        // (exact, Sterbenz), (double)baseIndex + mu == t exactly, so the reference's
+        // next time baseIndex + mu + advance (MuellerMuller.cs:113) is simply t + advance
+        double nt = static_cast<double>(base - d) + mu;
+        // the TED reuses the previous symbol widened to double and the previous
+        // decisions as sign masks: (double)(+-1) * x is exactly x with its sign flipped
         double psid = psi, psqd = psq;
+        uint32_t sdi = pdi >= 0.0f ? 0u : 0x80000000u, sdq = pdq >= 0.0f ? 0u : 0x80000000u;
+        auto flip = [](double v, uint32_t m) {
+            return __hiloint2double(__double2hiint(v) ^ static_cast<int>(m), __double2loint(v));
+        };
 #ifdef QPSK_LOOP_STAMPS
         unsigned long long c_bar = 0, c_loop = 0, c_iters = 0;
 #endif
@@ -192,84 +226,81 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 row[0] = row[kMir + kRing - 4]; row[1] = row[kMir + kRing - 3];
                 row[2] = row[kMir + kRing - 2]; row[3] = row[kMir + kRing - 1];
             }
-            const int rend = (r + 1) * kB < cnt ? (r + 1) * kB : cnt;
-            f2 *out = L.sym + ((r & 1) * SPW + lane) * kSymCap;
-            int kmax = stop ? 0 : (cap - nsym < kSymCap ? cap - nsym : kSymCap);
+            const int rend = (r + 1) * KB < cnt ? (r + 1) * KB : cnt;
+            d2 *out = L.sym + ((r & 1) * SPW + lane) * L.RS;
+            int kmax = stop ? 0 : (cap - nsym < CAP ? cap - nsym : CAP);
             int k = 0;
             const f2 *tp = taps(base);
             f2 xm1 = tp[0], x0 = tp[1], x1 = tp[2], x2 = tp[3];
+            // CubicLagrange4 (MuellerMuller.cs:160-190), float
+            auto interp = [&](float &ci, float &cq) {
+                const float t = static_cast<float>(mu);
+                const float tm1 = t - 1.0f, tm2 = t - 2.0f, tp1 = t + 1.0f;
+                const float cm1 = -(t * tm1 * tm2) * (1.0f / 6.0f);
+                const float c0 = (tp1 * tm1 * tm2) * (1.0f / 2.0f);
+                const float c1 = -(tp1 * t * tm2) * (1.0f / 2.0f);
+                const float c2 = (tp1 * t * tm1) * (1.0f / 6.0f);
+                ci = cm1 * xm1.x + c0 * x0.x + c1 * x1.x + c2 * x2.x;
+                cq = cm1 * xm1.y + c0 * x0.y + c1 * x1.y + c2 * x2.y;
+            };
+            // advance timing by adv (MuellerMuller.cs:113-115) and fetch the next taps
+            auto advance = [&](double adv) {
+                nt = nt + adv;
+                const double fl = floor(nt);
+                mu = nt - fl;
+                base = static_cast<int>(fl) + d;
+                tp = taps(base);
+                xm1 = tp[0]; x0 = tp[1]; x1 = tp[2]; x2 = tp[3];
+            };
             if (!has_prev && base + 2 < rend && kmax > 0) {
                 // very first symbol of the stream: no TED, advance = sps (MuellerMuller.cs:93-97)
-                const float t = static_cast<float>(mu);
-                const float tm1 = t - 1.0f, tm2 = t - 2.0f, tp1 = t + 1.0f;
-                const float cm1 = -(t * tm1 * tm2) * (1.0f / 6.0f);
-                const float c0 = (tp1 * tm1 * tm2) * (1.0f / 2.0f);
-                const float c1 = -(tp1 * t * tm2) * (1.0f / 2.0f);
-                const float c2 = (tp1 * t * tm1) * (1.0f / 6.0f);
-                const float ci = cm1 * xm1.x + c0 * x0.x + c1 * x1.x + c2 * x2.x;
-                const float cq = cm1 * xm1.y + c0 * x0.y + c1 * x1.y + c2 * x2.y;
+                float ci, cq;
+                interp(ci, cq);
                 has_prev = 1;
-                out[k++] = f2{ci, cq};
-                psi = ci; psq = cq;
                 psid = ci; psqd = cq;
-                pdi = ci >= 0.0f ? 1.0f : -1.0f;
-                pdq = cq >= 0.0f ? 1.0f : -1.0f;
-                const double nt = static_cast<double>(base - d) + mu + sps;
-                const double fl = floor(nt);
-                base = static_cast<int>(fl) + d;
-                mu = nt - fl;
-                tp = taps(base);
-                xm1 = tp[0]; x0 = tp[1]; x1 = tp[2]; x2 = tp[3];
+                out[k++] = d2{psid, psqd};
+                psi = ci; psq = cq;
+                sdi = ci >= 0.0f ? 0u : 0x80000000u;
+                sdq = cq >= 0.0f ? 0u : 0x80000000u;
+                advance(sps);
             }
-            while (base + 2 < rend && k < kmax) {
-                // CubicLagrange4 (MuellerMuller.cs:160-190), float
-                const float t = static_cast<float>(mu);
-                const float tm1 = t - 1.0f, tm2 = t - 2.0f, tp1 = t + 1.0f;
-                const float cm1 = -(t * tm1 * tm2) * (1.0f / 6.0f);
-                const float c0 = (tp1 * tm1 * tm2) * (1.0f / 2.0f);
-                const float c1 = -(tp1 * t * tm2) * (1.0f / 2.0f);
-                const float c2 = (tp1 * t * tm1) * (1.0f / 6.0f);
-                const float ci = cm1 * xm1.x + c0 * x0.x + c1 * x1.x + c2 * x2.x;
-                const float cq = cm1 * xm1.y + c0 * x0.y + c1 * x1.y + c2 * x2.y;
-                // M&M TED (MuellerMuller.cs:78-80): decisions are +-1, so each
-                // (double)d * x product is exactly +-x
+            auto step = [&]() {
+                float ci, cq;
+                interp(ci, cq);
+                // M&M TED (MuellerMuller.cs:78-80)
+                const uint32_t si = ci >= 0.0f ? 0u : 0x80000000u;
+                const uint32_t sq = cq >= 0.0f ? 0u : 0x80000000u;
                 const double cid = ci, cqd = cq;
-                const double t1 = (pdi >= 0.0f ? cid : -cid) + (pdq >= 0.0f ? cqd : -cqd);
-                const double t2 = (ci >= 0.0f ? psid : -psid) + (cq >= 0.0f ? psqd : -psqd);
+                const double t1 = flip(cid, sdi) + flip(cqd, sdq);
+                const double t2 = flip(psid, si) + flip(psqd, sq);
                 const double e = t1 - t2;
-                // PI filter, clamp, advance (MuellerMuller.cs:83-91)
+                // PI filter, clamp, advance (MuellerMuller.cs:83-91); the clamp
+                // rarely engages once locked, so it sits behind a branch
                 integ = integ + ki * e;
                 double corr = kp * e + integ;
-                corr = corr > 0.1 ? 0.1 : corr;
-                corr = corr < -0.1 ? -0.1 : corr;
-                const double adv = sps + corr;
-                out[k++] = f2{ci, cq};
-                psi = ci; psq = cq;
+                if (__builtin_expect(fabs(corr) > 0.1, 0)) corr = corr > 0.1 ? 0.1 : -0.1;
+                out[k++] = d2{cid, cqd};
                 psid = cid; psqd = cqd;
-                pdi = ci >= 0.0f ? 1.0f : -1.0f;
-                pdq = cq >= 0.0f ? 1.0f : -1.0f;
-                const double nt = static_cast<double>(base - d) + mu + adv;   // :113-115
-                const double fl = floor(nt);
-                base = static_cast<int>(fl) + d;
-                mu = nt - fl;
-                tp = taps(base);
-                xm1 = tp[0]; x0 = tp[1]; x1 = tp[2]; x2 = tp[3];
+                sdi = si; sdq = sq;
+                advance(sps + corr);
 #ifdef QPSK_LOOP_STAMPS
                 ++c_iters;
 #endif
+            };
+            // k < kmax also bounds a stream whose timing went NaN (base stuck)
+            while (base + 2 < rend && k < kmax) step();
+            if (k > 0) {
+                psi = static_cast<float>(psid);
+                psq = static_cast<float>(psqd);
             }
             nsym += k;
+            pdi = sdi ? -1.0f : 1.0f;
+            pdq = sdq ? -1.0f : 1.0f;
             if (!stop && nsym >= cap && base + 2 < rend) {
                 // MuellerMuller.cs:73-102: the symbol after the last one that fits
                 // still runs the TED/PI update, then the call stops
-                const float t = static_cast<float>(mu);
-                const float tm1 = t - 1.0f, tm2 = t - 2.0f, tp1 = t + 1.0f;
-                const float cm1 = -(t * tm1 * tm2) * (1.0f / 6.0f);
-                const float c0 = (tp1 * tm1 * tm2) * (1.0f / 2.0f);
-                const float c1 = -(tp1 * t * tm2) * (1.0f / 2.0f);
-                const float c2 = (tp1 * t * tm1) * (1.0f / 6.0f);
-                const float ci = cm1 * xm1.x + c0 * x0.x + c1 * x1.x + c2 * x2.x;
-                const float cq = cm1 * xm1.y + c0 * x0.y + c1 * x1.y + c2 * x2.y;
+                float ci, cq;
+                interp(ci, cq);
                 const float di = ci >= 0.0f ? 1.0f : -1.0f;
                 const float dq = cq >= 0.0f ? 1.0f : -1.0f;
                 if (has_prev) {
@@ -280,7 +311,14 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 has_prev = 1;
                 stop = true;
             }
+            // the Costas wave runs `kfull` symbols as a uniform loop (no per-lane
+            // exit masks) and only the remainder with per-lane counts.  A round
+            // that lies inside a stream's samples holds at least
+            // floor(64 / (sps + 0.1)) symbol instants (the timing advance is at
+            // most sps + 0.1); one vote tells whether every stream reached it.
+            const bool short_round = __ballot(mine && k < kfull) != 0;
             if (lane < SPW) L.cnt[(r & 3) * SPW + lane] = k;
+            if (lane == 0) L.cnt[4 * SPW + (r & 3)] = short_round ? 0 : kfull;
             ACC(c_loop, tl);
         }
 #ifdef QPSK_LOOP_STAMPS
@@ -332,6 +370,9 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         const double ca = P.c_alpha, cb = P.c_beta;
         const double kTwoPi = 2.0 * 3.14159265358979311600;
         const double kPi = 3.14159265358979311600;
+        // sincos argument: theta itself unless a wrap left |theta| > 1e6
+        // (qpsk_sincos_arg), so the per-symbol path has no range branch
+        double xr = qpsk_sincos_arg(theta);
 #ifdef QPSK_LOOP_STAMPS
         unsigned long long k_bar = 0, k_loop = 0;
 #endif
@@ -342,27 +383,39 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             if (r == 0 || r > NR) continue;
             STAMP(tl);
             const int slot = (r - 1) & 1;
+            const int mlo = __builtin_amdgcn_readfirstlane(L.cnt[4 * SPW + ((r - 1) & 3)]);
+            if (lane >= SPW) continue;   // exec = the batch's lanes for the whole round
             const int m = mine ? L.cnt[((r - 1) & 3) * SPW + lane] : 0;
-            const f2 *in = L.sym + (slot * SPW + lane) * kSymCap;
-            f2 *out = L.rot + (slot * SPW + lane) * kSymCap;
-            f2 y = in[0];
-            for (int k = 0; k < m; ++k) {
-                const f2 yn = in[k + 1];   // next symbol, read under this one's chain
-                // CostasLoopQpsk.cs:63-92: double NCO, float I/O
+            const d2 *in = L.sym + (slot * SPW + lane) * L.RS;
+            f2 *out = L.rot + (slot * SPW + lane) * L.RS;
+            d2 y = in[0];
+            auto step = [&](int k) {
+                const d2 yn = in[k + 1];   // next symbol, read under this one's chain
+                // CostasLoopQpsk.cs:63-92: double NCO, float I/O (y already widened)
                 double sn, cs;
-                qpsk_sincos(theta, &sn, &cs);
-                const double mi = static_cast<double>(y.x) * cs + static_cast<double>(y.y) * sn;
-                const double mq = static_cast<double>(y.y) * cs - static_cast<double>(y.x) * sn;
+                qpsk_sincos_tab_core(xr, L.tab, L.tab_lo, &sn, &cs);
+                const double mi = y.x * cs + y.y * sn;
+                const double mq = y.y * cs - y.x * sn;
                 const float ri = static_cast<float>(mi), rq = static_cast<float>(mq);
-                // (double)e * m with e = +-1 is exact: a sign flip gives the same number
-                const double pe = (ri >= 0.0f ? mq : -mq) - (rq >= 0.0f ? mi : -mi);
+                // e = +-1 (GetSign, :52-56): e*m is exact, so fma(ei, mq, -(eq*mi))
+                // rounds the same exact difference as the reference's subtraction
+                const double ei = ri >= 0.0f ? 1.0 : -1.0;
+                const double eq = rq >= 0.0f ? 1.0 : -1.0;
+                const double pe = fma(ei, mq, -(eq * mi));
                 freq = freq + cb * pe;
                 theta = theta + (freq + ca * pe);
-                if (__builtin_expect(fabs(theta) > kPi, 0))        // CostasLoopQpsk.cs:89-91
+                xr = theta;
+                if (__builtin_expect(fabs(theta) > kPi, 0)) {      // CostasLoopQpsk.cs:89-91
                     theta = theta > kPi ? theta - kTwoPi : theta + kTwoPi;
+                    xr = qpsk_sincos_arg(theta);
+                }
                 out[k] = f2{ri, rq};
                 y = yn;
-            }
+            };
+            int k = 0;
+#pragma unroll 2
+            for (; k < mlo; ++k) step(k);       // uniform trip count
+            for (; k < m; ++k) step(k);         // per-lane remainder (~1 symbol)
             ACC(k_loop, tl);
         }
 #ifdef QPSK_LOOP_STAMPS
@@ -397,7 +450,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         if (r < 2) continue;
         const int slot = (r - 2) & 1;
         const int m = mine ? L.cnt[((r - 2) & 3) * SPW + lane] : 0;
-        const f2 *in = L.rot + (slot * SPW + lane) * kSymCap;
+        const f2 *in = L.rot + (slot * SPW + lane) * L.RS;
         for (int k = 0; k < m; ++k) {
             const f2 rr = in[k];
             if (SYMS) {
@@ -457,33 +510,40 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     if (a.n_bits) a.n_bits[s] = MODE == kModeDemodulate ? nbits : 0;
 }
 
-template <int SPW>
+template <int SPW, int CAP, int KB>
 static void launch_loop_spw(const LoopArgs &a, const LoopParams &P, int mode, hipStream_t stream) {
     dim3 grid((a.S + SPW - 1) / SPW), block(256);
     const bool syms = a.syms != nullptr;
     const bool diff = P.differential != 0;
     if (mode == kModeConstellation)
-        hipLaunchKernelGGL((loop_kernel<kModeConstellation, false, true, SPW>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeConstellation, false, true, SPW, CAP, KB>), grid, block, 0, stream, a, P);
     else if (diff && syms)
-        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, true, SPW>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, true, SPW, CAP, KB>), grid, block, 0, stream, a, P);
     else if (diff)
-        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, false, SPW>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, false, SPW, CAP, KB>), grid, block, 0, stream, a, P);
     else if (syms)
-        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, true, SPW>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, true, SPW, CAP, KB>), grid, block, 0, stream, a, P);
     else
-        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, false, SPW>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, false, SPW, CAP, KB>), grid, block, 0, stream, a, P);
 }
 
-void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int streams_per_block,
+void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant,
                  hipStream_t stream) {
     hipLaunchKernelGGL(carry_prefix_kernel, dim3(a.S), dim3(64), 0, stream, a);
-    // the loop is latency-bound per stream and a wave's lanes are free, so
-    // 32 streams per workgroup; measured faster than 16 even at S=256, where
-    // only 8 CUs are busy (profiles/r01_loop_probe.txt)
-    if (streams_per_block == 16)
-        launch_loop_spw<16>(a, P, mode, stream);
+    // The loop is latency-bound per stream; a wave's lanes are free, so the
+    // default (sps >= 2) is 32 streams x 64-sample rounds.  Measured at C2
+    // (profiles/r01_loop_probe.txt): 16 x 64 and 16 x 128 (half the barriers)
+    // both run slower per symbol.  sps < 2 needs the 80-symbol round capacity,
+    // which fits LDS at 16 streams x 64.  variant (qpsk_demod_params.loop_variant)
+    // forces 1 = 16 x 64, 2 = 32 x 64, 3 = 16 x 128; all compute identical results.
+    if (P.sps < 2.0)
+        launch_loop_spw<16, kCapAny, 64>(a, P, mode, stream);
+    else if (variant == 1)
+        launch_loop_spw<16, kCapSps2, 64>(a, P, mode, stream);
+    else if (variant == 3)
+        launch_loop_spw<16, kCap128Sps2, 128>(a, P, mode, stream);
     else
-        launch_loop_spw<32>(a, P, mode, stream);
+        launch_loop_spw<32, kCapSps2, 64>(a, P, mode, stream);
 }
 
 }  // namespace qpsk

@@ -66,6 +66,7 @@ struct qpsk_demod {
     LoopDesign d;
     TapsRev taps{};
     LoopParams lp{};
+    int loop_variant = 0;
     FllParams fp{};
     hipStream_t stream = nullptr;
     bool own_stream = false;
@@ -141,6 +142,10 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
         delete h;
         return fail(QPSK_ERR_ARGUMENT, "vector_lanes must be 1, 4, 8 or 16");
     }
+    if (p->loop_variant < 0 || p->loop_variant > 3) {
+        delete h;
+        return fail(QPSK_ERR_ARGUMENT, "loop_variant must be 0..3");
+    }
     std::string err;
     int rc = design_loops(p->sample_rate, p->symbol_rate, p->rrc_alpha, p->rrc_span,
                           p->symbol_sync_bandwidth, p->costas_loop_bandwidth, p->cfo_loop_bandwidth,
@@ -157,6 +162,7 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
     h->lp.c_alpha = h->d.costas_alpha;
     h->lp.c_beta = h->d.costas_beta;
     h->lp.differential = p->differential ? 1 : 0;
+    h->loop_variant = p->loop_variant;
     h->fp.beta = h->d.fll_beta;
     h->fp.alpha = h->d.fll_alpha;
     h->fp.max_freq = h->d.fll_max_freq;
@@ -390,7 +396,7 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
     la.syms_cap = h->syms_cap;
     la.n_syms = h->d_counts + S;
     la.S = S;
-    launch_loop(la, h->lp, mode, 0, st);
+    launch_loop(la, h->lp, mode, h->loop_variant, st);
     HIP_TRY(hipGetLastError());
     if (ev) HIP_TRY(hipEventRecord(ev[4], st));
 

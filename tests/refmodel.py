@@ -150,10 +150,39 @@ def _fma(a, b, c):
     return float(Fraction(a) * Fraction(b) + Fraction(c))
 
 
-_S = [-1.66666666666666324348e-01, 8.33333333332248946124e-03, -1.98412698298579493134e-04,
-      2.75573137070700676789e-06, -2.50507602534068634195e-08, 1.58969099521155010221e-10]
-_C = [4.16666666666666019037e-02, -1.38888888888741095749e-03, 2.48015872894767294178e-05,
-      -2.75573143513906633035e-07, 2.08757232129817482790e-09, -1.13596475577881948265e-11]
+# The table is recomputed here independently of tools/gen_sincos_table.py
+# (different pi source and series grouping): sin/cos(k pi/256) as a correctly
+# rounded double head plus the tail rounded to float.
+_PI_DIGITS = "3.14159265358979323846264338327950288419716939937510582097494459230781640628620899"
+
+
+def _table():
+    from decimal import Decimal, localcontext
+    out = []
+    with localcontext() as ctx:
+        ctx.prec = 70
+        pi = Decimal(_PI_DIGITS)
+        for k in range(512):
+            a = pi * k / 256
+            # sin and cos from one pass over the exp series terms a^n/n!
+            term, sn, cs, n = Decimal(1), Decimal(0), Decimal(0), 0
+            while n < 90:
+                cs += term if n % 4 == 0 else (-term if n % 4 == 2 else 0)
+                sn += term if n % 4 == 1 else (-term if n % 4 == 3 else 0)
+                n += 1
+                term = term * a / n
+            row = []
+            for v in (sn, cs):
+                if abs(v) < Decimal("1e-40"):
+                    row += [0.0, 0.0]
+                else:
+                    hi = float(v)
+                    row += [hi, float(np.float32(float(v - Decimal(hi))))]
+            out.append(tuple(row))
+    return out
+
+
+SINCOS_TABLE = _table()
 
 
 def portable_sincos(x):
@@ -161,23 +190,16 @@ def portable_sincos(x):
         if math.isnan(x) or math.isinf(x):
             return math.nan, math.nan
         x = math.fmod(x, 6.28318530717958647693)
-    k = float(round(x * 6.36619772367581382433e-01))  # rint: half-even
-    r = _fma(-k, 1.57079632679489655800e+00, x)
-    r = _fma(-k, 6.12323399573676603587e-17, r)
-    r = _fma(-k, -1.49738490485916983e-33, r)
+    k = float(round(x * float.fromhex("0x1.45f306dc9c883p+6")))  # rint: half-even
+    r = _fma(-k, float.fromhex("0x1.921fb54442d18p-7"), x)
+    r = _fma(-k, float.fromhex("0x1.1a62633145c07p-61"), r)
+    r = _fma(-k, float.fromhex("-0x1.f1976b7ed8fbcp-117"), r)
+    ts, ls, tc, lc = SINCOS_TABLE[int(k) & 511]
     z = r * r
-    zz = z * z
-    sa, sb, sc = _fma(z, _S[1], _S[0]), _fma(z, _S[3], _S[2]), _fma(z, _S[5], _S[4])
-    ps = _fma(zz, _fma(zz, sc, sb), sa)
-    v = z * r
-    ks = _fma(v, ps, r)
-    ca, cb, cc = _fma(z, _C[1], _C[0]), _fma(z, _C[3], _C[2]), _fma(z, _C[5], _C[4])
-    pc = _fma(zz, _fma(zz, cc, cb), ca)
-    hz = 0.5 * z
-    w = 1.0 - hz
-    kc = w + (((1.0 - w) - hz) + zz * pc)
-    q = int(k) & 3
-    return [(ks, kc), (kc, -ks), (-ks, -kc), (-kc, ks)][q]
+    r3p = (r * z) * _fma(z, 1.0 / 120.0, -1.0 / 6.0)
+    cm = z * _fma(z, _fma(z, -1.0 / 720.0, 1.0 / 24.0), -0.5)
+    return (ts + _fma(tc, r, _fma(tc, r3p, _fma(ts, cm, ls))),
+            tc + _fma(-ts, r, _fma(-ts, r3p, _fma(tc, cm, lc))))
 
 
 class Costas:

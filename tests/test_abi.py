@@ -167,3 +167,38 @@ int main() {
                            "-I", os.path.join(ROOT, "qpsk-modulator-demodulator_amd", "csrc"),
                            str(src), "-o", str(exe)])
     assert subprocess.check_output([str(exe)]).decode().strip() == "0"
+
+
+def _header_floats(path, macro):
+    import re
+    text = open(path).read()
+    body = text.split(f"#define {macro} \\", 1)[1].split("#define", 1)[0]
+    vals = []
+    for tok in re.findall(r"-?0x[0-9a-fA-F.]+p[+-]?\d+f?|-?0\.0f?", body):
+        vals.append(float.fromhex(tok.rstrip("f")))
+    return vals
+
+
+def test_sincos_tables_match_independent_model():
+    """Product and oracle table headers are identical and equal the table the
+    numpy model recomputes on its own (tests/refmodel.py)."""
+    import refmodel as RM
+    prod = os.path.join(ROOT, "qpsk-modulator-demodulator_amd", "csrc", "qpsk_sincos_table.h")
+    orc = os.path.join(ROOT, "oracle", "or_sincos_table.h")
+    hi_p, lo_p = _header_floats(prod, "QPSK_SINCOS_TAB_VALUES_HI"), _header_floats(prod, "QPSK_SINCOS_TAB_VALUES_LO")
+    hi_o, lo_o = _header_floats(orc, "OR_SINCOS_TAB_VALUES_HI"), _header_floats(orc, "OR_SINCOS_TAB_VALUES_LO")
+    assert hi_p == hi_o and lo_p == lo_o and len(hi_p) == 1024 and len(lo_p) == 1024
+    ref = [v for ts, ls, tc, lc in RM.SINCOS_TABLE for v in (ts, tc)]
+    ref_lo = [v for ts, ls, tc, lc in RM.SINCOS_TABLE for v in (ls, lc)]
+    assert hi_p == ref and lo_p == ref_lo
+
+
+@pytest.mark.parametrize("kw", [dict(loop_variant=4), dict(loop_variant=-1), dict(vector_lanes=3),
+                                dict(max_samples_per_call=0)])
+def test_create_rejects_bad_knobs_before_touching_a_device(kw):
+    """Argument checks run before any HIP call, so they hold on a CPU-only host."""
+    import ctypes as C
+    args = dict(sample_rate=K.FS, symbol_rate=K.FS // 8, rrc_alpha=0.4, rrc_span=8)
+    args.update(kw)
+    h = C.c_void_p()
+    assert Q.lib().qpsk_demod_create(C.byref(Q.params(**args)), 4, C.byref(h)) == Q.QPSK_ERR_ARGUMENT

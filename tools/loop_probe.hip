@@ -10,7 +10,7 @@ using namespace qpsk;
 int main(int argc, char** argv) {
   const int S = argc > 1 ? atoi(argv[1]) : 256;
   const int64_t n = argc > 2 ? atoll(argv[2]) : (1 << 20);
-  const int spw = argc > 3 ? atoi(argv[3]) : 16;
+  const int spw = argc > 3 ? atoi(argv[3]) : 0;   // loop_variant: 0 auto, 1 16x64, 2 32x64, 3 16x128
   const int64_t stride = ((kMfPrefix + n + 2 + 63) / 64) * 64;
   std::vector<float> h(2 * stride * (size_t)S);
   std::mt19937 g(1); std::normal_distribution<float> nd(0.f, 0.3f);
@@ -33,12 +33,12 @@ int main(int argc, char** argv) {
   float ms; hipEventElapsedTime(&ms, e0, e1);
   std::vector<unsigned long long> pr(8 * S); hipMemcpy(pr.data(), probe, pr.size() * 8, hipMemcpyDeviceToHost);
   int64_t ns; hipMemcpy(&ns, cnt + S, 8, hipMemcpyDeviceToHost);
-  printf("S=%d n=%lld spw=%d: %.3f ms, stream0 symbols %lld -> %.1f ns/symbol\n", S, (long long)n, spw, ms, (long long)ns, ms * 1e6 / ns);
+  printf("S=%d n=%lld variant=%d: %.3f ms, stream0 symbols %lld -> %.1f ns/symbol\n", S, (long long)n, spw, ms, (long long)ns, ms * 1e6 / ns);
   for (int b = 0; b < 3; ++b) {
     auto* p = &pr[8 * b];
     const double R = (double)p[7];
-    printf(" WG %d rounds %llu: per round cycles: loader wait %.0f bar %.0f | M&M bar %.0f loop %.0f | Costas bar %.0f loop %.0f | M&M cyc/sym %.0f\n",
-           b, p[7], p[0] / R, p[1] / R, p[2] / R, p[3] / R, p[5] / R, p[6] / R, (double)p[3] / p[4]);
+    printf(" WG %d rounds %llu: per round cycles: loader wait %.0f bar %.0f | M&M bar %.0f loop %.0f | Costas bar %.0f loop %.0f | cyc/sym M&M %.0f Costas %.0f\n",
+           b, p[7], p[0] / R, p[1] / R, p[2] / R, p[3] / R, p[5] / R, p[6] / R, (double)p[3] / p[4], (double)p[6] / p[4]);
   }
   return 0;
 }
