@@ -41,7 +41,7 @@ constexpr int lds_slots(int n) { return n + ((n >> 6) << 3) + 8; }
 constexpr int kFirThreads = 256;
 
 template <int T, int W, int Q, bool VEC>
-__global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRev taps) {
+__global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRev taps, const float *hrev) {
     constexpr int TILE = kFirThreads * Q;
     constexpr int NIN = TILE + T - 1;
     constexpr int J = T / W;          // full Vector<float> blocks
@@ -96,6 +96,18 @@ __global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRe
         if (lo == hi) return row[c + 8 * lo];
         return row[c + 8 * lo + ((r + (c & 63)) >= 64 ? 8 : 0)];
     };
+    // Long filters (T > 80): the taps no longer fit in SGPRs next to everything
+    // else and hipcc spills them through v_writelane/v_readlane (+26 % VALU at
+    // T = 129).  Instead each lane phase l loads only its own J taps (uniform
+    // loads from the device copy) after a compiler barrier, so at most J taps
+    // are live at a time.
+    constexpr bool kPhasedTaps = true;
+    typedef __attribute__((address_space(4))) const float cfloat;   // scalar (s_load) path
+    cfloat *hc = (cfloat *)hrev;
+    auto tap = [&](int idx) -> float {
+        if constexpr (kPhasedTaps) return hc[idx];
+        else return taps.h[idx];
+    };
     f2 acc[Q];
     if constexpr (J == 0) {
 #pragma unroll
@@ -103,6 +115,7 @@ __global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRe
     }
 #pragma unroll
     for (int l = 0; l < W && J > 0; ++l) {
+        if constexpr (kPhasedTaps) asm volatile("" ::: "memory");
         // Lane accumulator l of every output: sum_j hrev[jW+l] * x[t-T+1+jW+l],
         // j ascending (FIRFilter.cs:165-174); u_i = x[t0 + l + W i] is shared by
         // the Q outputs of this thread.
@@ -114,7 +127,7 @@ __global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRe
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 const int j = i - q;
-                if (j >= 0 && j < J) p[q] = taps.h[j * W + l] * u;
+                if (j >= 0 && j < J) p[q] = tap(j * W + l) * u;
             }
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
@@ -131,7 +144,7 @@ __global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRe
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const f2 u = rd(W * q + NVEC + k);
-            acc[q] = acc[q] + taps.h[NVEC + k] * u;
+            acc[q] = acc[q] + tap(NVEC + k) * u;
         }
     }
     __syncthreads();
@@ -292,15 +305,15 @@ __global__ __launch_bounds__(64) void fll_kernel(FllArgs a, FllParams P) {
 // Launchers
 // ---------------------------------------------------------------------------
 template <int T>
-static bool launch_fir_w8(const FirArgs &a, const TapsRev &taps, int S, int64_t n_max, bool vec,
-                          hipStream_t stream) {
+static bool launch_fir_w8(const FirArgs &a, const TapsRev &taps, const float *hrev, int S,
+                          int64_t n_max, bool vec, hipStream_t stream) {
     constexpr int Q = 8;
     const int64_t tiles = (n_max + kFirThreads * Q - 1) / (kFirThreads * Q);
     dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(S));
     if (vec)
-        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, true>), grid, dim3(kFirThreads), 0, stream, a, taps);
+        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, true>), grid, dim3(kFirThreads), 0, stream, a, taps, hrev);
     else
-        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, false>), grid, dim3(kFirThreads), 0, stream, a, taps);
+        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, false>), grid, dim3(kFirThreads), 0, stream, a, taps, hrev);
     return true;
 }
 
@@ -312,15 +325,15 @@ bool launch_fir(const FirArgs &a, const TapsRev &taps, const float *hrev_dev, in
                      (a.y_stride % 2 == 0) && (a.y_offset % 2 == 0);
     if (W == 8) {
         switch (T) {
-        case 13: return launch_fir_w8<13>(a, taps, S, n_max, vec, stream);
-        case 17: return launch_fir_w8<17>(a, taps, S, n_max, vec, stream);
-        case 21: return launch_fir_w8<21>(a, taps, S, n_max, vec, stream);
-        case 33: return launch_fir_w8<33>(a, taps, S, n_max, vec, stream);
-        case 41: return launch_fir_w8<41>(a, taps, S, n_max, vec, stream);
-        case 49: return launch_fir_w8<49>(a, taps, S, n_max, vec, stream);
-        case 65: return launch_fir_w8<65>(a, taps, S, n_max, vec, stream);
-        case 97: return launch_fir_w8<97>(a, taps, S, n_max, vec, stream);
-        case 129: return launch_fir_w8<129>(a, taps, S, n_max, vec, stream);
+        case 13: return launch_fir_w8<13>(a, taps, hrev_dev, S, n_max, vec, stream);
+        case 17: return launch_fir_w8<17>(a, taps, hrev_dev, S, n_max, vec, stream);
+        case 21: return launch_fir_w8<21>(a, taps, hrev_dev, S, n_max, vec, stream);
+        case 33: return launch_fir_w8<33>(a, taps, hrev_dev, S, n_max, vec, stream);
+        case 41: return launch_fir_w8<41>(a, taps, hrev_dev, S, n_max, vec, stream);
+        case 49: return launch_fir_w8<49>(a, taps, hrev_dev, S, n_max, vec, stream);
+        case 65: return launch_fir_w8<65>(a, taps, hrev_dev, S, n_max, vec, stream);
+        case 97: return launch_fir_w8<97>(a, taps, hrev_dev, S, n_max, vec, stream);
+        case 129: return launch_fir_w8<129>(a, taps, hrev_dev, S, n_max, vec, stream);
         default: break;
         }
     }
