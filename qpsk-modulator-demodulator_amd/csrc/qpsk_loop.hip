@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "qpsk_kernels.h"
 #include "qpsk_sincos.h"
@@ -99,11 +100,11 @@ struct RowStride { static constexpr int value = CAP + 1; };
 template <int SPW, int CAP, int KB>
 struct LoopLds {
     static constexpr int RS = RowStride<CAP>::value;
+    double tab[1024];              // sincos table head (qpsk_sincos.h), at LDS offset 0 so
+    double tab_lo[1024];           // the table index is the whole address; tail (floats, widened)
     f2 mf[SPW * Ring<KB>::row];    // sample ring   [stream][mirror | 4 rounds x KB]
     d2 sym[2 * SPW * RS];          // M&M -> Costas [slot][stream][RS], widened to double
     f2 rot[2 * SPW * RS];          // Costas -> decode
-    double tab[1024];              // sincos table head (qpsk_sincos.h)
-    double tab_lo[1024];           // sincos table tail (float values, widened)
     int cnt[4 * SPW + 4];          // symbols produced by the M&M in round r: cnt[r & 3];
                                    // cnt[4*SPW + (r & 3)] = their minimum over the batch
 };
@@ -146,8 +147,40 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         const int c2 = 2 * (lane % (KB / 2));
         const f2 *mf = reinterpret_cast<const f2 *>(a.mf);
         const bool lo_half = lane < KB / 2;
+        // Fast path (every round but a stream's last): byte offsets of each
+        // stream's queue relative to the workgroup's first MF row, computed once
+        // and kept in VGPRs, so a round costs one SGPR base update plus, per
+        // stream, M0 + one global_load_lds (no per-stream readlanes or bounds
+        // tests).  Rows past the batch reuse stream 0's offsets (in bounds).
+        const int blk_s0 = blockIdx.x * SPW;
+        const f2 *wg_mf = mf + static_cast<int64_t>(blk_s0) * a.mf_stride;
+        const int nvalid = a.S - blk_s0 < SPW ? a.S - blk_s0 : SPW;
+        uint32_t voff[SPW];
+#pragma unroll
+        for (int j = 0; j < SPW; ++j) {
+            const int jj = j < nvalid ? j : 0;
+            const int64_t oj = readlane64(org, jj) - static_cast<int64_t>(blk_s0) * a.mf_stride;
+            voff[j] = static_cast<uint32_t>((oj + c2) * 8);
+        }
+        // the fast path needs every stream of the workgroup to hold the whole round
+        int cmin = valid ? cnt : 0x7fffffff;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const int w = __shfl_xor(cmin, o, 64);
+            cmin = w < cmin ? w : cmin;
+        }
+        cmin = __builtin_amdgcn_readfirstlane(cmin);
         auto issue = [&](int r) {
             const int roff = (r & 3) * KB;
+            if ((r + 1) * KB <= cmin) {
+                const char *rb = reinterpret_cast<const char *>(wg_mf + static_cast<int64_t>(r) * KB);
+#pragma unroll
+                for (int j = 0; j < SPW; ++j)
+                    if (lo_half)
+                        __builtin_amdgcn_global_load_lds((glb_void_t *)(rb + voff[j]),
+                                                         (lds_void_t *)(L.mf + j * kRowS + kMir + roff), 16, 0, 0);
+                return;
+            }
 #pragma unroll 4
             for (int j = 0; j < SPW; ++j) {
                 const int c = __builtin_amdgcn_readlane(cnt, j);
@@ -162,7 +195,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             }
         };
 #ifdef QPSK_LOOP_STAMPS
-        unsigned long long t_wait = 0, t_bar = 0;
+        unsigned long long t_wait = 0, t_bar = 0, t_issue = 0;
 #endif
         if (NR > 0) issue(0);
         if (NR > 1) issue(1);
@@ -174,12 +207,14 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             STAMP(tb);
             __builtin_amdgcn_s_barrier();
             ACC(t_bar, tb);
+            STAMP(ti);
             if (r + 2 < NR) issue(r + 2);
+            ACC(t_issue, ti);
         }
 #ifdef QPSK_LOOP_STAMPS
         if (a.probe && lane == 0) {
             a.probe[blockIdx.x * 8 + 0] = t_wait;
-            a.probe[blockIdx.x * 8 + 1] = t_bar;
+            a.probe[blockIdx.x * 8 + 1] = t_bar + (t_issue << 32);
         }
 #endif
         return;
@@ -201,6 +236,23 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         f2 *row = L.mf + lane * kRowS;
         // taps x[b-1..b+2] of physical index b: contiguous thanks to the mirror
         auto taps = [&](int b) -> const f2 * { return row + kMir - 3 + ((b + 2) & (kRing - 1)); };
+        // the same address straight from floor(t): fl + (1.5*2^52 + d + 2) holds
+        // b + 2 in its low mantissa bits (no float->int conversion on the chain)
+        const double tap_shift = 6755399441055744.0 + static_cast<double>(d + 2);
+        // loop-invariant LDS address of x[-3] relative to the ring, kept opaque so
+        // the whole base lives in one VGPR and the tap reads use immediate offsets
+        typedef __attribute__((address_space(3))) const f2 lds_f2;
+        uint32_t tap0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_f2 *)(row + kMir - 3)));
+        asm volatile("" : "+v"(tap0));
+        auto taps_fl = [&](double fl) -> lds_f2 * {
+            union { double v; unsigned long long u; } kb;
+            kb.v = fl + tap_shift;
+            const uint32_t addr = tap0 + 8u * (static_cast<uint32_t>(kb.u) & (kRing - 1));
+            return reinterpret_cast<lds_f2 *>(static_cast<uintptr_t>(addr));
+        };
+        // symbols that start in every 64-sample round once a stream is inside its
+        // samples: the timing advance is at most sps + 0.1 per symbol
+        const int kguar = static_cast<int>(floor((KB - sps - 4.0) / (sps + 0.1)));
         // logical time baseIndex + mu.  After baseIndex = floor(t), mu = t - baseIndex
         // (exact, Sterbenz), (double)baseIndex + mu == t exactly, so the reference's
         // next time baseIndex + mu + advance (MuellerMuller.cs:113) is simply t + advance
@@ -230,7 +282,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             d2 *out = L.sym + ((r & 1) * SPW + lane) * L.RS;
             int kmax = stop ? 0 : (cap - nsym < CAP ? cap - nsym : CAP);
             int k = 0;
-            const f2 *tp = taps(base);
+            lds_f2 *tp = (lds_f2 *)taps(base);
             f2 xm1 = tp[0], x0 = tp[1], x1 = tp[2], x2 = tp[3];
             // CubicLagrange4 (MuellerMuller.cs:160-190), float
             auto interp = [&](float &ci, float &cq) {
@@ -249,7 +301,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const double fl = floor(nt);
                 mu = nt - fl;
                 base = static_cast<int>(fl) + d;
-                tp = taps(base);
+                tp = taps_fl(fl);
                 xm1 = tp[0]; x0 = tp[1]; x1 = tp[2]; x2 = tp[3];
             };
             if (!has_prev && base + 2 < rend && kmax > 0) {
@@ -274,11 +326,11 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const double t1 = flip(cid, sdi) + flip(cqd, sdq);
                 const double t2 = flip(psid, si) + flip(psqd, sq);
                 const double e = t1 - t2;
-                // PI filter, clamp, advance (MuellerMuller.cs:83-91); the clamp
-                // rarely engages once locked, so it sits behind a branch
+                // PI filter, clamp, advance (MuellerMuller.cs:83-91); the clamp as
+                // a select: |c| > 0.1 -> copysign(0.1, c); NaN stays NaN as in C#
                 integ = integ + ki * e;
-                double corr = kp * e + integ;
-                if (__builtin_expect(fabs(corr) > 0.1, 0)) corr = corr > 0.1 ? 0.1 : -0.1;
+                const double c = kp * e + integ;
+                const double corr = fabs(c) > 0.1 ? copysign(0.1, c) : c;
                 out[k++] = d2{cid, cqd};
                 psid = cid; psqd = cqd;
                 sdi = si; sdq = sq;
@@ -287,6 +339,17 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 ++c_iters;
 #endif
             };
+            // Every batch stream that is inside its samples starts at least kguar
+            // symbols in this round, unless its capacity or timing says otherwise:
+            // one vote lets the wave run those with a uniform trip count (no
+            // per-lane exit masks), then the per-lane loop finishes the round.
+            {
+                const double room = static_cast<double>(rend - d - 3) - nt;   // t + d + 2 < rend - 1
+                const bool short_lane = !(room >= kguar * (sps + 0.1)) || kmax - k < kguar;
+                const int kg = __builtin_amdgcn_readfirstlane(__ballot(mine && short_lane) == 0 ? kguar : 0);
+                if (lane < SPW)   // lanes past the batch have no row
+                    for (int u = 0; u < kg; ++u) step();
+            }
             // k < kmax also bounds a stream whose timing went NaN (base stuck)
             while (base + 2 < rend && k < kmax) step();
             if (k > 0) {
@@ -370,9 +433,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         const double ca = P.c_alpha, cb = P.c_beta;
         const double kTwoPi = 2.0 * 3.14159265358979311600;
         const double kPi = 3.14159265358979311600;
-        // sincos argument: theta itself unless a wrap left |theta| > 1e6
-        // (qpsk_sincos_arg), so the per-symbol path has no range branch
-        double xr = qpsk_sincos_arg(theta);
 #ifdef QPSK_LOOP_STAMPS
         unsigned long long k_bar = 0, k_loop = 0;
 #endif
@@ -388,12 +448,15 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             const int m = mine ? L.cnt[((r - 1) & 3) * SPW + lane] : 0;
             const d2 *in = L.sym + (slot * SPW + lane) * L.RS;
             f2 *out = L.rot + (slot * SPW + lane) * L.RS;
-            d2 y = in[0];
-            auto step = [&](int k) {
+            d2 y;
+            // CostasLoopQpsk.cs:63-92: double NCO, float I/O (y already widened).
+            // HUGE: theta may exceed the table reduction's range (qpsk_sincos_arg);
+            // the fast pass assumes it does not and the round is redone if it did.
+            auto step = [&](int k, auto huge) {
                 const d2 yn = in[k + 1];   // next symbol, read under this one's chain
-                // CostasLoopQpsk.cs:63-92: double NCO, float I/O (y already widened)
                 double sn, cs;
-                qpsk_sincos_tab_core(xr, L.tab, L.tab_lo, &sn, &cs);
+                if constexpr (decltype(huge)::value) qpsk_sincos_tab(theta, L.tab, L.tab_lo, &sn, &cs);
+                else qpsk_sincos_tab_core(theta, L.tab, L.tab_lo, &sn, &cs);
                 const double mi = y.x * cs + y.y * sn;
                 const double mq = y.y * cs - y.x * sn;
                 const float ri = static_cast<float>(mi), rq = static_cast<float>(mq);
@@ -403,19 +466,34 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const double eq = rq >= 0.0f ? 1.0 : -1.0;
                 const double pe = fma(ei, mq, -(eq * mi));
                 freq = freq + cb * pe;
-                theta = theta + (freq + ca * pe);
-                xr = theta;
-                if (__builtin_expect(fabs(theta) > kPi, 0)) {      // CostasLoopQpsk.cs:89-91
-                    theta = theta > kPi ? theta - kTwoPi : theta + kTwoPi;
-                    xr = qpsk_sincos_arg(theta);
-                }
+                const double tn = theta + (freq + ca * pe);
+                // single +-2pi wrap (:89-91) as a select: tn + copysign(2pi, -tn)
+                // is tn - 2pi above pi and tn + 2pi below -pi
+                const double tw = tn + copysign(kTwoPi, -tn);
+                theta = fabs(tn) > kPi ? tw : tn;
                 out[k] = f2{ri, rq};
                 y = yn;
             };
+            const double theta0 = theta, freq0 = freq;
+            y = in[0];
             int k = 0;
+            double amax = fabs(theta);   // largest sincos argument of the round
 #pragma unroll 2
-            for (; k < mlo; ++k) step(k);       // uniform trip count
-            for (; k < m; ++k) step(k);         // per-lane remainder (~1 symbol)
+            for (; k < mlo; ++k) {       // uniform trip count
+                step(k, std::false_type{});
+                amax = fmax(amax, fabs(theta));
+            }
+            for (; k < m; ++k) {         // per-lane remainder (~1 symbol)
+                step(k, std::false_type{});
+                amax = fmax(amax, fabs(theta));
+            }
+            // fmax drops NaN, which the fast path handles exactly like the full one
+            if (__builtin_expect(__ballot(mine && amax > 1.0e6) != 0, 0)) {
+                theta = theta0;
+                freq = freq0;
+                y = in[0];
+                for (k = 0; k < m; ++k) step(k, std::true_type{});
+            }
             ACC(k_loop, tl);
         }
 #ifdef QPSK_LOOP_STAMPS

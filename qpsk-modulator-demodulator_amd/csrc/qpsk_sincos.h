@@ -8,7 +8,8 @@
  * tests require the GPU Costas/FLL outputs to equal the oracle's bit for bit.
  *
  * Algorithm: Cody-Waite reduction by pi/256 with a three-part constant
- * (fma), a 512-entry table of correctly rounded sin/cos(k pi/256)
+ * (fma; the integer multiple comes from the 1.5*2^52 shifter, which also
+ * yields the table index), a 512-entry table of correctly rounded sin/cos(k pi/256)
  * (tools/gen_sincos_table.py), degree-5/6 Taylor polynomials for the residual
  * |r| <= pi/512 and angle addition with the table value added last.
  * Accuracy <= 1 ulp (table rounding + one final rounding).
@@ -52,23 +53,26 @@ QPSK_HD static inline double qpsk_sincos_arg(double x)
 QPSK_HD static inline void qpsk_sincos_tab_core(double x, const double *tab, const double *lo,
                                            double *s, double *c)
 {
-    const double INV = 0x1.45f306dc9c883p+6;      /* 256/pi */
-    const double P1 = 0x1.921fb54442d18p-7;       /* pi/256 rounded to double */
-    const double P2 = 0x1.1a62633145c07p-61;      /* next 53 bits */
-    const double P3 = -0x1.f1976b7ed8fbcp-117;    /* next bits */
+    const double INV = 0x1.45f306dc9c883p+6;       /* 256/pi */
+    const double SH = 0x1.8p+52;                   /* 1.5*2^52: ulp 1 */
+    const double P1 = 0x1.921fb54442d18p-7;        /* pi/256 rounded to double */
+    const double P2 = 0x1.1a62633145c07p-61;       /* next 53 bits */
+    const double P3 = -0x1.f1976b7ed8fbcp-117;     /* next bits */
     const double S3 = -0x1.5555555555555p-3, S5 = 0x1.1111111111111p-7;    /* -1/6, 1/120 */
     const double C4 = 0x1.5555555555555p-5, C6 = -0x1.6c16c16c16c17p-10;  /* 1/24, -1/720 */
-    const double k = rint(x * INV);
-    double r = fma(-k, P1, x);                    /* Cody-Waite: |r| <= pi/512 */
+    /* kb = x*256/pi + 1.5*2^52 rounds to an integer (ties to even), so
+     * k = kb - 1.5*2^52 = rint(x*256/pi) exactly (|x| <= 1e6) and the low
+     * mantissa bits of kb are k mod 512 in two's complement: the table index
+     * without a separate rint */
+    union { double d; unsigned long long u; } kb;
+    kb.d = x * INV + SH;
+    const double k = kb.d - SH;
+    double r = fma(-k, P1, x);                     /* Cody-Waite: |r| <= pi/512 */
     r = fma(-k, P2, r);
     r = fma(-k, P3, r);
-    /* table index = k mod 512: k + 1.5*2^52 puts the two's-complement low bits
-     * of the integer k in the low mantissa bits (|k| < 2^27 here) */
-    union { double d; unsigned long long u; } kb;
-    kb.d = k + 6755399441055744.0;
-    const unsigned i = (unsigned)(kb.u & 511u);
-    const double ts = tab[2 * i], tc = tab[2 * i + 1];
-    const double ls = lo[2 * i], lc = lo[2 * i + 1];
+    const unsigned i = (unsigned)(kb.u & 511u) * 2u;
+    const double ts = tab[i], tc = tab[i + 1];
+    const double ls = lo[i], lc = lo[i + 1];
     /* sin r = r + r^3(-1/6 + r^2/120), cos r - 1 = r^2(-1/2 + r^2/24 - r^4/720):
      * truncation < 1e-19 relative for |r| <= pi/512 */
     const double z = r * r;

@@ -236,3 +236,19 @@ def test_synth_generated_batch_parity_and_ber():
         r = np.frombuffer(txs[3000 + off:m + off].encode(), np.uint8)
         clean += int(np.count_nonzero(a != r) == 0)
     assert clean >= S // 2
+
+
+def test_huge_amplitude_takes_the_costas_rollback_path():
+    """Samples scaled by 1e12 drive theta far past the table reduction's range
+    (|theta| > 1e6): the loop kernel's fast pass detects it and redoes the round
+    with the full-range sincos, matching the oracle bit for bit."""
+    iq = K.batch_signals(3, seed0=300, sps=8, span=8, n_bits=800, snr_db=20) * np.float32(1e12)
+    n = iq.shape[1] // 2
+    calls = [[n // 3] * 3, [n - n // 3] * 3]
+    got, ref = gpu_run(iq, calls, 8, 8), oracle_run(iq, calls, 8, 8)
+    for ci, (ra, rb) in enumerate(zip(got, ref)):
+        for s, ((ba, sa), (bb, sb)) in enumerate(zip(ra, rb)):
+            assert ba == bb, f"call {ci} stream {s}: bits differ"
+            assert np.array_equal(sa.view(np.uint32), sb.view(np.uint32)), f"call {ci} stream {s}"
+    # (with |pe| ~ 1e12 the first symbol already moves freq by cb*pe ~ 1e10, so
+    # theta leaves [-1e6, 1e6] within a round)
