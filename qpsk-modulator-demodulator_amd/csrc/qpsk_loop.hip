@@ -257,15 +257,13 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         // (exact, Sterbenz), (double)baseIndex + mu == t exactly, so the reference's
         // next time baseIndex + mu + advance (MuellerMuller.cs:113) is simply t + advance
         double nt = static_cast<double>(base - d) + mu;
-        // the TED reuses the previous symbol widened to double and the previous
-        // decisions as sign masks: (double)(+-1) * x is exactly x with its sign flipped
+        // the TED reuses the previous symbol widened to double and the decisions
+        // as doubles +-1.0: d*x is exact, so fma(d1, x1, d2*x2) rounds the same
+        // exact sum as the reference's (double)d1*x1 + (double)d2*x2
         double psid = psi, psqd = psq;
-        uint32_t sdi = pdi >= 0.0f ? 0u : 0x80000000u, sdq = pdq >= 0.0f ? 0u : 0x80000000u;
-        auto flip = [](double v, uint32_t m) {
-            return __hiloint2double(__double2hiint(v) ^ static_cast<int>(m), __double2loint(v));
-        };
+        double pdid = pdi >= 0.0f ? 1.0 : -1.0, pdqd = pdq >= 0.0f ? 1.0 : -1.0;
 #ifdef QPSK_LOOP_STAMPS
-        unsigned long long c_bar = 0, c_loop = 0, c_iters = 0;
+        unsigned long long c_bar = 0, c_loop = 0, c_iters = 0, c_uni = 0;
 #endif
         for (int r = 0; r <= NR + 1; ++r) {
             STAMP(tb);
@@ -288,10 +286,15 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             auto interp = [&](float &ci, float &cq) {
                 const float t = static_cast<float>(mu);
                 const float tm1 = t - 1.0f, tm2 = t - 2.0f, tp1 = t + 1.0f;
-                const float cm1 = -(t * tm1 * tm2) * (1.0f / 6.0f);
-                const float c0 = (tp1 * tm1 * tm2) * (1.0f / 2.0f);
-                const float c1 = -(tp1 * t * tm2) * (1.0f / 2.0f);
-                const float c2 = (tp1 * t * tm1) * (1.0f / 6.0f);
+                // the reference's products, two per packed op:
+                //   cm1 = -((t*tm1)*tm2)/6  c0 = ((tp1*tm1)*tm2)/2
+                //   c1 = -((tp1*t)*tm2)/2   c2 = ((tp1*t)*tm1)/6
+                // (-x)*c == x*(-c) bit for bit, so the negations ride on the constants
+                const f2 bd = (f2{t, tp1} * tm1) * tm2;
+                const f2 fg = (tp1 * t) * f2{tm2, tm1};
+                const f2 c01 = bd * f2{-(1.0f / 6.0f), 1.0f / 2.0f};
+                const f2 c23 = fg * f2{-(1.0f / 2.0f), 1.0f / 6.0f};
+                const float cm1 = c01.x, c0 = c01.y, c1 = c23.x, c2 = c23.y;
                 ci = cm1 * xm1.x + c0 * x0.x + c1 * x1.x + c2 * x2.x;
                 cq = cm1 * xm1.y + c0 * x0.y + c1 * x1.y + c2 * x2.y;
             };
@@ -312,19 +315,19 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 psid = ci; psqd = cq;
                 out[k++] = d2{psid, psqd};
                 psi = ci; psq = cq;
-                sdi = ci >= 0.0f ? 0u : 0x80000000u;
-                sdq = cq >= 0.0f ? 0u : 0x80000000u;
+                pdid = ci >= 0.0f ? 1.0 : -1.0;
+                pdqd = cq >= 0.0f ? 1.0 : -1.0;
                 advance(sps);
             }
             auto step = [&]() {
                 float ci, cq;
                 interp(ci, cq);
                 // M&M TED (MuellerMuller.cs:78-80)
-                const uint32_t si = ci >= 0.0f ? 0u : 0x80000000u;
-                const uint32_t sq = cq >= 0.0f ? 0u : 0x80000000u;
+                const double did = ci >= 0.0f ? 1.0 : -1.0;
+                const double dqd = cq >= 0.0f ? 1.0 : -1.0;
                 const double cid = ci, cqd = cq;
-                const double t1 = flip(cid, sdi) + flip(cqd, sdq);
-                const double t2 = flip(psid, si) + flip(psqd, sq);
+                const double t1 = fma(pdid, cid, pdqd * cqd);
+                const double t2 = fma(did, psid, dqd * psqd);
                 const double e = t1 - t2;
                 // PI filter, clamp, advance (MuellerMuller.cs:83-91); the clamp as
                 // a select: |c| > 0.1 -> copysign(0.1, c); NaN stays NaN as in C#
@@ -333,22 +336,40 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const double corr = fabs(c) > 0.1 ? copysign(0.1, c) : c;
                 out[k++] = d2{cid, cqd};
                 psid = cid; psqd = cqd;
-                sdi = si; sdq = sq;
+                pdid = did; pdqd = dqd;
                 advance(sps + corr);
 #ifdef QPSK_LOOP_STAMPS
                 ++c_iters;
 #endif
             };
-            // Every batch stream that is inside its samples starts at least kguar
-            // symbols in this round, unless its capacity or timing says otherwise:
-            // one vote lets the wave run those with a uniform trip count (no
-            // per-lane exit masks), then the per-lane loop finishes the round.
+            // Symbols K = 0..G-1 of this round are certain to start while
+            // t + K (sps + 0.1) + d + 3 <= rend (the advance is at most sps + 0.1;
+            // one sample of margin absorbs rounding) and capacity allows.  Votes
+            // on the likely counts let the wave run the largest count every
+            // batch stream reaches as a uniform loop (no per-lane exit masks);
+            // the per-lane loop finishes the round.  NaN timing votes "short".
             {
-                const double room = static_cast<double>(rend - d - 3) - nt;   // t + d + 2 < rend - 1
-                const bool short_lane = !(room >= kguar * (sps + 0.1)) || kmax - k < kguar;
-                const int kg = __builtin_amdgcn_readfirstlane(__ballot(mine && short_lane) == 0 ? kguar : 0);
-                if (lane < SPW)   // lanes past the batch have no row
-                    for (int u = 0; u < kg; ++u) step();
+                const double room = static_cast<double>(rend - d - 3) - nt;
+                const double step_max = sps + 0.1;
+                const int cap_l = kmax - k;
+                auto reaches = [&](int G) { return room >= (G - 1) * step_max && cap_l >= G; };
+                int kg = 0;
+                if (__ballot(mine && !reaches(kguar + 2)) == 0) kg = kguar + 2;
+                else if (__ballot(mine && !reaches(kguar + 1)) == 0) kg = kguar + 1;
+                else if (__ballot(mine && !reaches(kguar)) == 0) kg = kguar;
+                kg = __builtin_amdgcn_readfirstlane(kg);
+                STAMP(tu);
+                if (lane < SPW) {  // lanes past the batch have no row
+                    // by two: the loop-carried symbol/decision registers alternate
+                    // instead of being copied back every symbol
+                    int u = 0;
+                    for (; u + 1 < kg; u += 2) {
+                        step();
+                        step();
+                    }
+                    if (u < kg) step();
+                }
+                ACC(c_uni, tu);
             }
             // k < kmax also bounds a stream whose timing went NaN (base stuck)
             while (base + 2 < rend && k < kmax) step();
@@ -357,8 +378,8 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 psq = static_cast<float>(psqd);
             }
             nsym += k;
-            pdi = sdi ? -1.0f : 1.0f;
-            pdq = sdq ? -1.0f : 1.0f;
+            pdi = static_cast<float>(pdid);
+            pdq = static_cast<float>(pdqd);
             if (!stop && nsym >= cap && base + 2 < rend) {
                 // MuellerMuller.cs:73-102: the symbol after the last one that fits
                 // still runs the TED/PI update, then the call stops
@@ -388,7 +409,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         if (a.probe && lane == 0) {
             a.probe[blockIdx.x * 8 + 2] = c_bar;
             a.probe[blockIdx.x * 8 + 3] = c_loop;
-            a.probe[blockIdx.x * 8 + 4] = c_iters;
+            a.probe[blockIdx.x * 8 + 4] = c_iters | (c_uni << 20);
             a.probe[blockIdx.x * 8 + 7] = NR;
         }
 #endif

@@ -37,8 +37,8 @@ int main(int argc, char** argv) {
   for (int b = 0; b < 3; ++b) {
     auto* p = &pr[8 * b];
     const double R = (double)p[7];
-    printf(" WG %d rounds %llu: per round cycles: loader wait %.0f bar %.0f issue %.0f | M&M bar %.0f loop %.0f | Costas bar %.0f loop %.0f | cyc/sym M&M %.0f Costas %.0f\n",
-           b, p[7], p[0] / R, (p[1] & 0xffffffffull) / R, (p[1] >> 32) / R, p[2] / R, p[3] / R, p[5] / R, p[6] / R, (double)p[3] / p[4], (double)p[6] / p[4]);
+    printf(" WG %d rounds %llu: per round cycles: loader wait %.0f bar %.0f issue %.0f | M&M bar %.0f loop %.0f | Costas bar %.0f loop %.0f | cyc/sym M&M %.0f Costas %.0f | M&M uniform-loop cycles/round %.0f\n",
+           b, p[7], p[0] / R, (p[1] & 0xffffffffull) / R, (p[1] >> 32) / R, p[2] / R, p[3] / R, p[5] / R, p[6] / R, (double)p[3] / (p[4] & 0xfffff), (double)p[6] / (p[4] & 0xfffff), (double)(p[4] >> 20) / R);
   }
   return 0;
 }
