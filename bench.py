@@ -170,6 +170,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo + --share-gpu rehearses the N>1 path on a one-GPU box")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="every rank uses cuda:0 (rehearsal only; numbers meaningless)")
     args = ap.parse_args()
 
     import torch
@@ -178,11 +182,14 @@ def main():
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", 0))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     cfg = dict(CONFIGS[args.config])
     S = args.streams or cfg["streams"]
@@ -234,7 +241,8 @@ def main():
     if rank == 0 and not args.no_parity:
         parity_ok = parity_check(iq, cfg, n)
     t_max, (errs, total_bits, lost, slips, bad) = reduce_stats(
-        elapsed, [errs, total_bits, lost, slips, 0 if parity_ok else 1], device=dev)
+        elapsed, [errs, total_bits, lost, slips, 0 if parity_ok else 1],
+        device=dev if args.dist_backend == "nccl" else None)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
