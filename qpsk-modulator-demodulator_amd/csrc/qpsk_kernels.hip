@@ -316,6 +316,14 @@ __global__ __launch_bounds__(64) void fll_kernel(FllArgs a, FllParams P) {
 // the same order as fll_kernel, so bit-identical.
 constexpr int kFll8Streams = 32;   // streams per 256-thread block
 
+// (a.x - b.x, a.y + b.y) in one v_pk_add_f32 (hipcc otherwise negates one lane
+// with a separate op and re-pairs the halves with v_mov)
+__device__ __forceinline__ f2 pk_sub_add(f2 a, f2 b) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 __global__ __launch_bounds__(256) void fll8_kernel(FllArgs a, FllParams P) {
     constexpr int N = kFllTaps;              // 40 = 5 blocks of 8
     constexpr int J = N / 8;
@@ -362,7 +370,7 @@ __global__ __launch_bounds__(256) void fll8_kernel(FllArgs a, FllParams P) {
         nmin = w2 < nmin ? w2 : nmin;
     }
     // one sample of one stream (Band-Edge Filter.cs:102-129), bit-identical to fll_kernel
-    auto sample = [&](int k, int64_t t) {
+    auto sample = [&](int k, int64_t t, bool first) {
         // older window samples (indices l + 8j <= 38 were written before this
         // sample); index 39 (j = 4, l = 7) is this sample's mix, below
         int start = pos + 1;
@@ -372,7 +380,16 @@ __global__ __launch_bounds__(256) void fll8_kernel(FllArgs a, FllParams P) {
         for (int j = 0; j < J; ++j) w[j] = ring[g][start + l + 8 * j];
         const f2 in = stage[g][k];
         float sn, cs;
-        qpsk_sincosf_tab(phase, tab, tab_lo, &sn, &cs);
+        // After a sample the phase is wrapped into [-2pi, 2pi] (or NaN), so only
+        // a call's first sample, with the stored phase, can need the |x| > 1e6
+        // pre-reduction; later samples use the table core directly.
+        if (first) qpsk_sincosf_tab(phase, tab, tab_lo, &sn, &cs);
+        else {
+            double sd, cd;
+            qpsk_sincos_tab_core(static_cast<double>(phase), tab, tab_lo, &sd, &cd);
+            sn = static_cast<float>(sd);
+            cs = static_cast<float>(cd);
+        }
         const float oi = in.x * cs - in.y * sn;
         const float oq = in.x * sn + in.y * cs;
         const f2 o = f2{oi, oq};
@@ -381,26 +398,28 @@ __global__ __launch_bounds__(256) void fll8_kernel(FllArgs a, FllParams P) {
         ring[g][pos] = o;
         ring[g][pos + N] = o;
         w[J - 1] = l == 7 ? o : w[J - 1];
-        // lane accumulator l of both filters (fll_dot, W = 8)
-        float ui = 0.f, uq = 0.f, li = 0.f, lq = 0.f;
+        // lane accumulator l of both filters (fll_dot, W = 8), I and Q packed:
+        // (hi*xr - hq*xi, hi*xi + hq*xr) = hi*(xr, xi) + (-(hq*xi), hq*xr)
+        f2 ua = f2{0.f, 0.f}, la = f2{0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < J; ++j) {
-            ui = ui + ((uhi[j] * w[j].x) - (uhq[j] * w[j].y));
-            uq = uq + ((uhi[j] * w[j].y) + (uhq[j] * w[j].x));
-            li = li + ((lhi[j] * w[j].x) - (lhq[j] * w[j].y));
-            lq = lq + ((lhi[j] * w[j].y) + (lhq[j] * w[j].x));
+            const f2 ws = f2{w[j].y, w[j].x};
+            const f2 ub = uhq[j] * ws, lb = lhq[j] * ws;
+            ua = ua + pk_sub_add(uhi[j] * w[j], ub);
+            la = la + pk_sub_add(lhi[j] * w[j], lb);
         }
-        accs[g][l] = make_float4(ui, uq, li, lq);
+        accs[g][l] = make_float4(ua.x, ua.y, la.x, la.y);
         asm volatile("" ::: "memory");   // group lanes write, then read each other's
-        float upi = 0.f, upq = 0.f, loi = 0.f, loq = 0.f;
+        f2 up = f2{0.f, 0.f}, lo = f2{0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < 8; ++q) {      // horizontal sum in lane order (:176-180)
             const float4 v = accs[g][q];
-            upi += v.x; upq += v.y; loi += v.z; loq += v.w;
+            up = up + f2{v.x, v.y};
+            lo = lo + f2{v.z, v.w};
         }
         asm volatile("" ::: "memory");
-        const float pu = upi * upi + upq * upq;
-        const float pl = loi * loi + loq * loq;
+        const float pu = up.x * up.x + up.y * up.y;
+        const float pl = lo.x * lo.x + lo.y * lo.y;
         const float err = pl - pu;
         freq += P.beta * err;
         phase += freq + P.alpha * err;
@@ -420,12 +439,14 @@ __global__ __launch_bounds__(256) void fll8_kernel(FllArgs a, FllParams P) {
         asm volatile("" ::: "memory");
         if (t0 + 8 <= nmin) {
             if (valid) {   // groups past the batch alias stream 0's rows: keep them out
+                if (t0 == 0) sample(0, 0, true);
+                else sample(0, t0, false);
 #pragma unroll
-                for (int k = 0; k < 8; ++k) sample(k, t0 + k);
+                for (int k = 1; k < 8; ++k) sample(k, t0 + k, false);
             }
         } else {
             for (int k = 0; k < 8; ++k)
-                if (t0 + k < n) sample(k, t0 + k);
+                if (t0 + k < n) sample(k, t0 + k, t0 + k == 0);
         }
         asm volatile("" ::: "memory");
     }
