@@ -159,6 +159,63 @@ def ber_after_lock(bits_dev, nbits_dev, tx_dev, n_streams, skip_bits=8000, windo
     return errs, total, lost, slips
 
 
+def split_gather(demod, fresh_state, iq_local, bits, nbits, S, n, world, rank, dev, synth_kw,
+                 backend):
+    """The RCCL leg of SURVEY.md §8e, measured after the no-collective bench:
+    rank 0 synthesises the whole batch and scatters the stream shards over
+    xGMI, every rank demodulates its shard, and rank 0 gathers the packed
+    bits and bit counts.  Returns per-phase times (max over ranks) and whether
+    every scattered shard equals the one the rank generated itself."""
+    import torch
+    import torch.distributed as dist
+    import qpsk_amd as Q
+    total_bytes = world * S * 2 * n * 4
+    if total_bytes > (48 << 30):
+        return {"skipped": f"whole batch {total_bytes / 2**30:.0f} GiB does not fit one GPU; "
+                           "each rank synthesises its own shard (no split)"}
+    host = backend != "nccl"          # gloo rehearsal: collectives on host tensors
+    full = None
+    if rank == 0:
+        full, _ = Q.synth_generate(world * S, n, FS, synth_kw["rs"], rrc_alpha=ALPHA,
+                                   rrc_span=synth_kw["span"], seed=0x5159534B, first_stream=0,
+                                   lo_ppm=1.0, cfo_hz=synth_kw["cfo"], multipath=synth_kw["mp"],
+                                   esn0_db=synth_kw["esn0"], device=dev.index)
+        if host:
+            full = full.cpu()
+    shard = torch.empty((S, 2 * n), dtype=torch.float32, device="cpu" if host else dev)
+    chunks = list(full.chunk(world, dim=0)) if rank == 0 else None
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    dist.scatter(shard, chunks, src=0)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    x = shard.to(dev) if host else shard
+    demod.set_state(fresh_state)
+    demod.process_device(x, n, bits, nbits)
+    torch.cuda.synchronize(dev)
+    t2 = time.perf_counter()
+    b, c = (bits.cpu(), nbits.cpu()) if host else (bits, nbits)
+    gb = [torch.empty_like(b) for _ in range(world)] if rank == 0 else None
+    gc = [torch.empty_like(c) for _ in range(world)] if rank == 0 else None
+    dist.gather(b, gb, dst=0)
+    dist.gather(c, gc, dst=0)
+    torch.cuda.synchronize(dev)
+    t3 = time.perf_counter()
+    same = int(torch.equal(x, iq_local))
+    del full, chunks
+    tt = torch.tensor([t1 - t0, t2 - t1, t3 - t2], dtype=torch.float64,
+                      device="cpu" if host else dev)
+    ok = torch.tensor([same], dtype=torch.int64, device="cpu" if host else dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    ts, td, tg = (float(v) for v in tt.tolist())
+    return {"scatter_ms": round(ts * 1e3, 3), "demod_ms": round(td * 1e3, 3),
+            "gather_ms": round(tg * 1e3, 3),
+            "value_with_split_gather": round(world * S * n / (ts + td + tg) / 1e6, 2),
+            "shards_match_local_synth": bool(ok.item())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -172,6 +229,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + --share-gpu rehearses the N>1 path on a one-GPU box")
+    ap.add_argument("--no-split-gather", action="store_true",
+                    help="skip the RCCL scatter/demod/gather pass that runs when N > 1")
     ap.add_argument("--share-gpu", action="store_true",
                     help="every rank uses cuda:0 (rehearsal only; numbers meaningless)")
     args = ap.parse_args()
@@ -244,6 +303,13 @@ def main():
         elapsed, [errs, total_bits, lost, slips, 0 if parity_ok else 1],
         device=dev if args.dist_backend == "nccl" else None)
 
+    sg = None
+    if world > 1 and not args.no_split_gather:
+        sg = split_gather(demod, fresh_state, iq, bits, nbits, S, n, world, rank, dev,
+                          dict(rs=rs, span=span, cfo=5000.0 if cfg["impaired"] else 0.0,
+                               mp=cfg["impaired"], esn0=20.0 if cfg["impaired"] else None),
+                          args.dist_backend)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # bounded sample: at most 512 streams (~10 s of CPU work at 2^20 samples)
@@ -262,7 +328,9 @@ def main():
     fir_bytes = 16.0 * S * n                      # 8 B in + 8 B out per complex sample
     fir_s = st["fir"] / 1e3
     achieved = fir_bytes / fir_s / 1e9 if fir_s > 0 else 0.0
-    traffic = load_traffic(args.config)
+    # the PMC passes were taken at the config's own shard size; any other
+    # size has no measured traffic
+    traffic = load_traffic(args.config) if (S == cfg["streams"] and n == 1 << 20) else None
     loop_bytes = (8.0 + 0.25 / sps) * S * n       # MF samples in + packed bits out
     out = {
         "metric": METRIC,
@@ -295,6 +363,8 @@ def main():
         "parity_vs_oracle": "bit-exact" if bad == 0 else "MISMATCH",
         "cpu_baseline": cpu,
     }
+    if sg is not None:
+        out["split_gather"] = sg
     if rank == 0:
         print(json.dumps(out), flush=True)
     demod.close()
