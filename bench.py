@@ -267,7 +267,10 @@ def main():
     p = Q.params(FS, rs, ALPHA, span, enable_fll=cfg["fll"], device=local, max_samples_per_call=n)
     demod = Q.BatchDemodulator(S, p)
     fresh_state = demod.get_state()   # for the BER pass (no second handle: C5 needs ~192 GiB)
-    stream = torch.cuda.current_stream(dev)
+    # a real stream (torch's legacy default is handle 0, which the C ABI reads
+    # as "library-owned"); torch ops and the demod then share one order
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     demod.set_stream(stream.cuda_stream)
     ms = demod.max_symbols(n)
     bits = torch.zeros((S, (2 * ms + 7) // 8 + 64), dtype=torch.uint8, device=dev)

@@ -156,6 +156,46 @@ int qpsk_framer_push(qpsk_framer *f, const uint8_t *bits, int64_t bits_stride_by
                      int64_t payload_stride, int64_t *n_payload);
 
 /* ---------------------------------------------------------------------------
+ * Device-resident framer and TSC search: the same
+ * DeModulateBytes state machine (QPSKDeModulator.cs:169-259) and TSC strip
+ * (:413-422), one workgroup per stream, fed straight from process()'s device
+ * bit rows with no host round trip.  Every pointer below is device memory and
+ * every call is ordered on the framer's stream.  The ring is a per-stream
+ * linear buffer of ring_capacity bytes (RingClear resets head to 0 and nothing
+ * consumes from the tail, so the reference ring never wraps inside a frame);
+ * overflow drops the frame and resyncs exactly like RingTryWriteByte (:95-103).
+ */
+typedef struct qpsk_framer_dev qpsk_framer_dev;
+/* ring_capacity <= 0 selects the reference's 300_000_000 bytes per stream (:58). */
+int qpsk_framer_dev_create(int32_t n_streams, const uint8_t *start_marker, int32_t n_start,
+                           const uint8_t *end_marker, int32_t n_end, int64_t ring_capacity,
+                           int32_t device, qpsk_framer_dev **out);
+int qpsk_framer_dev_destroy(qpsk_framer_dev *f);
+/* Bind to a caller-owned hipStream_t (NULL = library-owned stream). */
+int qpsk_framer_dev_set_stream(qpsk_framer_dev *f, void *hip_stream);
+/* Per-call markers (DeModulateBytes takes them per call); state is kept. */
+int qpsk_framer_dev_set_markers(qpsk_framer_dev *f, const uint8_t *start_marker, int32_t n_start,
+                                const uint8_t *end_marker, int32_t n_end);
+/* One DeModulateBytes step on every stream: bits rows as qpsk_demod_process
+ * wrote them, bit_offset[s] (NULL = 0) = first payload bit after the TSC, or
+ * < 0 when this call's TSC search failed (DeModulate returned ""); payload[s]
+ * receives the frame completed by this call (first payload_stride bytes) and
+ * n_payload[s] its full length (0 = none). */
+int qpsk_framer_dev_push(qpsk_framer_dev *f, const uint8_t *bits, int64_t bits_stride_bytes,
+                         const int64_t *bit_offset, const int64_t *n_bits, uint8_t *payload,
+                         int64_t payload_stride, int64_t *n_payload);
+/* Host copy of every stream's framer status (arrays of n_streams, any may be
+ * NULL; synchronises the framer's stream): in-frame flag, ring bytes held,
+ * start-hunt carry bits. */
+int qpsk_framer_dev_status(const qpsk_framer_dev *f, int32_t *in_frame, int64_t *ring_count,
+                           int64_t *carry_bits);
+/* qpsk_tsc_find for every stream of a device bit batch: offsets[s] = bit index
+ * just past the first TSC occurrence in row s, -1 if absent, 0 for a NULL or
+ * blank tsc.  Ordered on hip_stream (NULL = the null stream). */
+int qpsk_tsc_find_device(const uint8_t *bits, int64_t bits_stride_bytes, const int64_t *n_bits,
+                         int32_t n_streams, const char *tsc, int64_t *offsets, void *hip_stream);
+
+/* ---------------------------------------------------------------------------
  * Synthetic batched input (QPSKModulator.Modulate + the test bench channel),
  * generated in device memory.  Stream s draws its payload from
  * splitmix64(seed ^ s); tx_bits receives the payload bits (packed MSB-first).

@@ -58,6 +58,11 @@ int dev_alloc(T **p, size_t count) {
 }
 }  // namespace
 
+namespace qpsk {
+// shared error channel for the other C-ABI translation units (framer, synth)
+int set_last_error(int code, const std::string &msg) { return fail(code, msg); }
+}  // namespace qpsk
+
 struct qpsk_demod {
     qpsk_demod_params p{};
     int S = 0;

@@ -123,6 +123,16 @@ def lib():
     L.qpsk_demod_design.argtypes = [C.POINTER(DemodParams), _f32p, C.c_int32, _f64p, _f32p, _f32p]
     L.qpsk_framer_push.argtypes = [C.c_void_p, _u8p, C.c_int64, _i64p, _i64p, _u8p, C.c_int64,
                                    _i64p]
+    L.qpsk_framer_dev_create.argtypes = [C.c_int32, _u8p, C.c_int32, _u8p, C.c_int32, C.c_int64,
+                                         C.c_int32, C.POINTER(C.c_void_p)]
+    L.qpsk_framer_dev_destroy.argtypes = [C.c_void_p]
+    L.qpsk_framer_dev_set_stream.argtypes = [C.c_void_p, C.c_void_p]
+    L.qpsk_framer_dev_set_markers.argtypes = [C.c_void_p, _u8p, C.c_int32, _u8p, C.c_int32]
+    L.qpsk_framer_dev_push.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_int64, C.c_void_p]
+    L.qpsk_framer_dev_status.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.qpsk_tsc_find_device.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_char_p,
+                                       C.c_void_p, C.c_void_p]
     L.qpsk_synth_params_init.argtypes = [C.POINTER(SynthParams), C.c_int32, C.c_int32]
     L.qpsk_synth_generate.argtypes = [C.POINTER(SynthParams), C.c_int32, C.c_void_p, C.c_int32,
                                       C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]
@@ -136,7 +146,9 @@ EXPORTED_SYMBOLS = [
     "qpsk_tsc_find", "qpsk_demod_enable_timing", "qpsk_demod_stage_times", "qpsk_demod_rrc_taps",
     "qpsk_demod_gains", "qpsk_demod_fll_taps", "qpsk_demod_state_bytes", "qpsk_demod_get_state",
     "qpsk_demod_set_state", "qpsk_demod_design", "qpsk_framer_create", "qpsk_framer_destroy",
-    "qpsk_framer_set_markers", "qpsk_framer_push",
+    "qpsk_framer_set_markers", "qpsk_framer_push", "qpsk_framer_dev_create",
+    "qpsk_framer_dev_destroy", "qpsk_framer_dev_set_stream", "qpsk_framer_dev_set_markers",
+    "qpsk_framer_dev_push", "qpsk_framer_dev_status", "qpsk_tsc_find_device",
     "qpsk_synth_params_init", "qpsk_synth_generate",
 ]
 
@@ -355,6 +367,67 @@ class Framer:
     def __del__(self):
         if getattr(self, "_h", None):
             lib().qpsk_framer_destroy(self._h)
+            self._h = None
+
+
+def _markers(start: bytes, end: bytes):
+    if len(start) == 0:
+        raise ValueError("startMarker cannot be empty.")                          # :174
+    if len(end) == 0:
+        raise ValueError("endMarker cannot be empty.")                            # :175
+    return (np.frombuffer(bytes(start), dtype=np.uint8).copy(),
+            np.frombuffer(bytes(end), dtype=np.uint8).copy())
+
+
+def tsc_find_device(bits_dev, n_bits_dev, tsc: str | None, offsets_dev, hip_stream=None):
+    """qpsk_tsc_find on every row of a device bit batch (torch CUDA tensors);
+    offsets_dev[s] = first payload bit after the TSC, -1 if absent."""
+    _check(lib().qpsk_tsc_find_device(
+        bits_dev.data_ptr(), bits_dev.stride(0) * bits_dev.element_size(), n_bits_dev.data_ptr(),
+        int(bits_dev.shape[0]), tsc.encode() if tsc else None, offsets_dev.data_ptr(),
+        hip_stream))
+
+
+class DeviceFramer:
+    """The DeModulateBytes framer (QPSKDeModulator.cs:169-259) resident on the
+    GPU: fed straight from BatchDemodulator.process_device's bit rows."""
+
+    def __init__(self, n_streams, start: bytes, end: bytes, ring_capacity=300_000_000, device=0):
+        s, e = _markers(start, end)
+        self.S = n_streams
+        h = C.c_void_p()
+        _check(lib().qpsk_framer_dev_create(n_streams, s.ctypes.data_as(_u8p), s.size,
+                                            e.ctypes.data_as(_u8p), e.size, int(ring_capacity),
+                                            int(device), C.byref(h)))
+        self._h = h
+
+    def set_stream(self, hip_stream_ptr: int | None):
+        _check(lib().qpsk_framer_dev_set_stream(self._h, hip_stream_ptr))
+
+    def set_markers(self, start: bytes, end: bytes):
+        s, e = _markers(start, end)
+        _check(lib().qpsk_framer_dev_set_markers(self._h, s.ctypes.data_as(_u8p), s.size,
+                                                 e.ctypes.data_as(_u8p), e.size))
+
+    def push(self, bits_dev, n_bits_dev, payload_dev, n_payload_dev, offsets_dev=None):
+        """Stream-ordered; every argument a torch CUDA tensor (payload_dev is
+        [S][payload_stride] uint8, n_payload_dev [S] int64)."""
+        _check(lib().qpsk_framer_dev_push(
+            self._h, bits_dev.data_ptr(), bits_dev.stride(0) * bits_dev.element_size(),
+            offsets_dev.data_ptr() if offsets_dev is not None else None, n_bits_dev.data_ptr(),
+            payload_dev.data_ptr(), payload_dev.stride(0), n_payload_dev.data_ptr()))
+
+    def status(self):
+        inf = np.zeros(self.S, np.int32)
+        cnt = np.zeros(self.S, np.int64)
+        car = np.zeros(self.S, np.int64)
+        _check(lib().qpsk_framer_dev_status(self._h, inf.ctypes.data, cnt.ctypes.data,
+                                            car.ctypes.data))
+        return inf, cnt, car
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().qpsk_framer_dev_destroy(self._h)
             self._h = None
 
 

@@ -393,3 +393,86 @@ class FLL:
             elif self.freq < -self.maxf:
                 self.freq = -self.maxf
         return out.reshape(-1)
+
+
+# ---------------------------------------------------------------------------
+# Byte framer, on '0'/'1' strings exactly as the C# walks them
+# (QPSKDeModulator.cs:57-259, HelperFunctions.cs:32-70).
+
+def bits_to_bytes(bits: str, off: int) -> bytes:
+    """BitPacker.BitsToBytes: MSB-first from bit `off`, trailing partial byte dropped."""
+    n = (len(bits) - off) // 8
+    if len(bits) - off < 8:
+        return b""
+    return int(bits[off:off + 8 * n], 2).to_bytes(n, "big")
+
+
+class RefFramer:
+    """One reference instance's framer fields and DeModulateBytes step, fed the
+    post-TSC bit string of each call (rxBits, :178)."""
+
+    def __init__(self, ring_capacity=300_000_000):
+        self.cap = ring_capacity
+        self.reset()
+
+    def reset(self):                       # ResetFramer (:159-167)
+        self.in_frame = False
+        self.locked = -1
+        self.carry = ""
+        self.ring = bytearray()
+        self.pack_byte = 0
+        self.pack_bits = 0
+
+    def _append(self, bits: str) -> int:   # AppendBitsToRing (:108-129)
+        produced = 0
+        for c in bits:
+            self.pack_byte = ((self.pack_byte << 1) | (c == "1")) & 0xFF
+            self.pack_bits += 1
+            if self.pack_bits == 8:
+                if len(self.ring) >= self.cap:
+                    return -1
+                self.ring.append(self.pack_byte)
+                produced += 1
+                self.pack_bits = 0
+                self.pack_byte = 0
+        return produced
+
+    def _finish(self, appended: int, end: bytes) -> bytes:
+        frm = max(0, len(self.ring) - (appended + len(end)))
+        at = bytes(self.ring).find(end, frm)       # RingIndexOf (:133-149)
+        if at >= 0:
+            out = bytes(self.ring[:at])
+            self.reset()
+            return out
+        return b""
+
+    def push(self, rx: str, start: bytes, end: bytes) -> bytes:
+        if not rx:
+            return b""                              # :179-180
+        if not self.in_frame:
+            cand = self.carry + rx
+            for off in range(8):                    # :187-230
+                by = bits_to_bytes(cand, off)
+                s = by.find(start)
+                if not by or s < 0:
+                    continue
+                mend = off + 8 * (s + len(start))
+                if mend > len(cand):
+                    continue
+                self.in_frame = True
+                self.locked = off
+                self.ring = bytearray()
+                self.pack_byte = self.pack_bits = 0
+                appended = self._append(cand[mend:])
+                if appended < 0:
+                    self.reset()
+                    return b""
+                return self._finish(appended, end)
+            keep = min(len(cand), len(start) * 8 + 7)   # :233-235
+            self.carry = cand[len(cand) - keep:] if keep else ""
+            return b""
+        appended = self._append(rx)
+        if appended < 0:
+            self.reset()
+            return b""
+        return self._finish(appended, end)
