@@ -216,6 +216,41 @@ def split_gather(demod, fresh_state, iq_local, bits, nbits, S, n, world, rank, d
             "shards_match_local_synth": bool(ok.item())}
 
 
+TSC_BITS = "11001010011101100100100110101100" + "01110100111001011010001101101001"  # testAtDataLevel.cs:20-22
+
+
+def framer_pass(bits, nbits, S, stream, reps=5):
+    """§8f rank 1, measured beside the headline (never inside it): the device
+    TSC search + DeModulateBytes framer over the bit rows the chain just
+    produced, timed with HIP events on the framer's stream."""
+    import torch
+    import qpsk_amd as Q
+    fr = Q.DeviceFramer(S, b"\x02", b"\x03", ring_capacity=1 << 16, device=bits.device.index)
+    fr.set_stream(stream.cuda_stream)
+    offs = torch.zeros(S, dtype=torch.int64, device=bits.device)
+    pay = torch.zeros((S, 256), dtype=torch.uint8, device=bits.device)
+    npay = torch.zeros(S, dtype=torch.int64, device=bits.device)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    t_tsc = t_push = 0.0
+    frames = 0
+    for r in range(reps + 1):
+        ev[0].record(stream)
+        Q.tsc_find_device(bits, nbits, TSC_BITS, offs, stream.cuda_stream)
+        ev[1].record(stream)
+        fr.push(bits, nbits, pay, npay, None)
+        ev[2].record(stream)
+        stream.synchronize()
+        if r:                                  # first pass allocates the hunt scratch
+            t_tsc += ev[0].elapsed_time(ev[1])
+            t_push += ev[1].elapsed_time(ev[2])
+            frames += int((npay > 0).sum().item())
+    row_bytes = float(nbits.sum().item()) / 8
+    del fr
+    return {"tsc_ms": round(t_tsc / reps, 4), "framer_ms": round(t_push / reps, 4),
+            "frames_per_call": round(frames / reps, 1),
+            "bits_GBps": round(row_bytes / (t_push / reps * 1e-3) / 1e9, 1) if t_push > 0 else None}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -229,6 +264,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + --share-gpu rehearses the N>1 path on a one-GPU box")
+    ap.add_argument("--no-framer", action="store_true",
+                    help="skip the device TSC + framer pass measured beside the headline")
     ap.add_argument("--no-split-gather", action="store_true",
                     help="skip the RCCL scatter/demod/gather pass that runs when N > 1")
     ap.add_argument("--share-gpu", action="store_true",
@@ -306,6 +343,8 @@ def main():
         elapsed, [errs, total_bits, lost, slips, 0 if parity_ok else 1],
         device=dev if args.dist_backend == "nccl" else None)
 
+    fr_stats = framer_pass(bits, nbits, S, stream) if not args.no_framer else None
+
     sg = None
     if world > 1 and not args.no_split_gather:
         sg = split_gather(demod, fresh_state, iq, bits, nbits, S, n, world, rank, dev,
@@ -366,6 +405,8 @@ def main():
         "parity_vs_oracle": "bit-exact" if bad == 0 else "MISMATCH",
         "cpu_baseline": cpu,
     }
+    if fr_stats is not None:
+        out["framer"] = fr_stats
     if sg is not None:
         out["split_gather"] = sg
     if rank == 0:
