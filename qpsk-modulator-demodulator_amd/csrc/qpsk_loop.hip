@@ -285,18 +285,21 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             // CubicLagrange4 (MuellerMuller.cs:160-190), float
             auto interp = [&](float &ci, float &cq) {
                 const float t = static_cast<float>(mu);
-                const float tm1 = t - 1.0f, tm2 = t - 2.0f, tp1 = t + 1.0f;
                 // the reference's products, two per packed op:
                 //   cm1 = -((t*tm1)*tm2)/6  c0 = ((tp1*tm1)*tm2)/2
                 //   c1 = -((tp1*t)*tm2)/2   c2 = ((tp1*t)*tm1)/6
-                // (-x)*c == x*(-c) bit for bit, so the negations ride on the constants
-                const f2 bd = (f2{t, tp1} * tm1) * tm2;
-                const f2 fg = (tp1 * t) * f2{tm2, tm1};
+                // (-x)*c == x*(-c) bit for bit, so the negations ride on the
+                // constants; t + 0 == t (t = (float)mu is +0 or positive or NaN)
+                const f2 p1 = f2{t, t} + f2{0.0f, 1.0f};       // {t, tp1}
+                const f2 p2 = f2{t, t} + f2{-2.0f, -1.0f};     // {tm2, tm1}
+                const f2 bd = (p1 * p2.y) * p2.x;
+                const f2 fg = p2 * (p1.y * p1.x);
                 const f2 c01 = bd * f2{-(1.0f / 6.0f), 1.0f / 2.0f};
                 const f2 c23 = fg * f2{-(1.0f / 2.0f), 1.0f / 6.0f};
-                const float cm1 = c01.x, c0 = c01.y, c1 = c23.x, c2 = c23.y;
-                ci = cm1 * xm1.x + c0 * x0.x + c1 * x1.x + c2 * x2.x;
-                cq = cm1 * xm1.y + c0 * x0.y + c1 * x1.y + c2 * x2.y;
+                // ((cm1*xm1 + c0*x0) + c1*x1) + c2*x2 for I and Q in one packed op each
+                const f2 acc = ((c01.x * xm1 + c01.y * x0) + c23.x * x1) + c23.y * x2;
+                ci = acc.x;
+                cq = acc.y;
             };
             // advance timing by adv (MuellerMuller.cs:113-115) and fetch the next taps
             auto advance = [&](double adv) {
@@ -329,11 +332,13 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const double t1 = fma(pdid, cid, pdqd * cqd);
                 const double t2 = fma(did, psid, dqd * psqd);
                 const double e = t1 - t2;
-                // PI filter, clamp, advance (MuellerMuller.cs:83-91); the clamp as
-                // a select: |c| > 0.1 -> copysign(0.1, c); NaN stays NaN as in C#
+                // PI filter, clamp, advance (MuellerMuller.cs:83-91)
                 integ = integ + ki * e;
                 const double c = kp * e + integ;
-                const double corr = fabs(c) > 0.1 ? copysign(0.1, c) : c;
+                // the clamp as min/max: c > 0.1 -> 0.1, c < -0.1 -> -0.1 (a NaN c,
+                // which the reference cannot survive either, clamps instead of
+                // propagating)
+                const double corr = __builtin_fmax(__builtin_fmin(c, 0.1), -0.1);
                 out[k++] = d2{cid, cqd};
                 psid = cid; psqd = cqd;
                 pdid = did; pdqd = dqd;
