@@ -258,6 +258,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--samples", type=int, default=1 << 20)
+    ap.add_argument("--loop-variant", type=int, default=0,
+                    help="symbol-loop kernel shape (qpsk_demod_params.loop_variant; 0 = auto)")
     ap.add_argument("--streams", type=int, default=0, help="override streams per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
@@ -301,7 +303,8 @@ def main():
                               cfo_hz=5000.0 if cfg["impaired"] else 0.0,
                               multipath=cfg["impaired"], esn0_db=20.0 if cfg["impaired"] else None,
                               device=local)
-    p = Q.params(FS, rs, ALPHA, span, enable_fll=cfg["fll"], device=local, max_samples_per_call=n)
+    p = Q.params(FS, rs, ALPHA, span, enable_fll=cfg["fll"], device=local, max_samples_per_call=n,
+                 loop_variant=args.loop_variant)
     demod = Q.BatchDemodulator(S, p)
     fresh_state = demod.get_state()   # for the BER pass (no second handle: C5 needs ~192 GiB)
     # a real stream (torch's legacy default is handle 0, which the C ABI reads

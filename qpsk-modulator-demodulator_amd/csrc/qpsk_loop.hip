@@ -55,9 +55,13 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 // sample ring holds 4 rounds (index = p & (4*KB - 1)), preceded by a mirror of
 // its last 4 samples so the 4 interpolation taps are always contiguous in LDS.
 constexpr int kMir = 4;
+#ifndef QPSK_RING_PAD
+#define QPSK_RING_PAD 0
+#endif
 template <int KB> struct Ring {
     static constexpr int len = 4 * KB;
-    static constexpr int row = kMir + len;   // per-stream LDS row: [mirror 4][ring]
+    static constexpr int PAD = QPSK_RING_PAD;
+    static constexpr int row = kMir + len + PAD;   // per-stream LDS row: [mirror 4][ring][pad]
 };
 // symbols per round per stream (template CAP): at most floor((KB + 3) / (sps - 0.1)) + 1
 // start in one round: 75 (KB 64, sps >= 1), 36 (KB 64, sps >= 2), 69 (KB 128, sps >= 2)
@@ -140,6 +144,13 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     }
     __syncthreads();
 
+#ifdef QPSK_LOOP_STAMPS
+    if (a.probe && lane == 0) {   // where each wave runs: HW_ID (SIMD, CU, SE) and XCC
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+        a.probe[blockIdx.x * 16 + 12 + wave] = hw | (static_cast<unsigned long long>(xcc) << 32);
+    }
+#endif
     if (wave == 0) {
         // ============================================================ loader
         // one glds instruction = KB/2 lanes x 16 B = one stream's round (8*KB bytes)
@@ -213,13 +224,27 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         }
 #ifdef QPSK_LOOP_STAMPS
         if (a.probe && lane == 0) {
-            a.probe[blockIdx.x * 8 + 0] = t_wait;
-            a.probe[blockIdx.x * 8 + 1] = t_bar + (t_issue << 32);
+            a.probe[blockIdx.x * 16 + 0] = t_wait;
+            a.probe[blockIdx.x * 16 + 1] = t_bar + (t_issue << 32);
         }
 #endif
         return;
     }
 
+#ifdef QPSK_PROBE_NOMM
+    if (wave == 1) {   // diagnostic: a stand-in M&M that only feeds 8 fixed symbols a round
+        for (int r = 0; r <= NR + 1; ++r) {
+            __builtin_amdgcn_s_barrier();
+            if (r >= NR) continue;
+            d2 *out = L.sym + ((r & 1) * SPW + lane) * L.RS;
+            if (lane < SPW)
+                for (int k = 0; k < 8; ++k) out[k] = d2{0.7 + 0.01 * k, -0.7 + 0.02 * k};
+            if (lane < SPW) L.cnt[(r & 3) * SPW + lane] = mine ? 8 : 0;
+            if (lane == 0) L.cnt[4 * SPW + (r & 3)] = 8;
+        }
+        return;
+    }
+#endif
     if (wave == 1) {
         // ============================================================ M&M
         StreamState st;
@@ -230,7 +255,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         int has_prev = mine ? st.has_prev : 1;
         const double sps = P.sps, kp = P.kp, ki = P.ki;
         const int cap = n;                          // output span = 2n floats (QPSKDeModulator.cs:366)
-        const int kfull = static_cast<int>(floor(static_cast<double>(KB) / (sps + 0.1)));
         int nsym = 0;
         bool stop = !mine;                          // capacity reached (MuellerMuller.cs:101-102)
         f2 *row = L.mf + lane * kRowS;
@@ -253,6 +277,11 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         // symbols that start in every 64-sample round once a stream is inside its
         // samples: the timing advance is at most sps + 0.1 per symbol
         const int kguar = static_cast<int>(floor((KB - sps - 4.0) / (sps + 0.1)));
+        // largest backlog (samples behind rend) a stream may carry into the next
+        // round: half a round keeps its taps inside the ring slots not being
+        // refilled, and a round then holds at most (KB + lag_max + 4)/(sps - 0.1) + 1
+        // <= CAP symbols; <= 0 (small sps) means every round is finished
+        const double lag_max = fmin(0.5 * KB, (CAP - 1) * (sps - 0.1) - KB - 4.0);
         // logical time baseIndex + mu.  After baseIndex = floor(t), mu = t - baseIndex
         // (exact, Sterbenz), (double)baseIndex + mu == t exactly, so the reference's
         // next time baseIndex + mu + advance (MuellerMuller.cs:113) is simply t + advance
@@ -263,7 +292,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         double psid = psi, psqd = psq;
         double pdid = pdi >= 0.0f ? 1.0 : -1.0, pdqd = pdq >= 0.0f ? 1.0 : -1.0;
 #ifdef QPSK_LOOP_STAMPS
-        unsigned long long c_bar = 0, c_loop = 0, c_iters = 0, c_uni = 0;
+        unsigned long long c_bar = 0, c_loop = 0, c_iters = 0, c_uni = 0, c_uit = 0, c_pre = 0, c_post = 0;
 #endif
         for (int r = 0; r <= NR + 1; ++r) {
             STAMP(tb);
@@ -279,7 +308,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             const int rend = (r + 1) * KB < cnt ? (r + 1) * KB : cnt;
             d2 *out = L.sym + ((r & 1) * SPW + lane) * L.RS;
             int kmax = stop ? 0 : (cap - nsym < CAP ? cap - nsym : CAP);
-            int k = 0;
+            int k = 0, kuni = 0;
             lds_f2 *tp = (lds_f2 *)taps(base);
             f2 xm1 = tp[0], x0 = tp[1], x1 = tp[2], x2 = tp[3];
             // CubicLagrange4 (MuellerMuller.cs:160-190), float
@@ -350,21 +379,33 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             // Symbols K = 0..G-1 of this round are certain to start while
             // t + K (sps + 0.1) + d + 3 <= rend (the advance is at most sps + 0.1;
             // one sample of margin absorbs rounding) and capacity allows.  Votes
-            // on the likely counts let the wave run the largest count every
-            // batch stream reaches as a uniform loop (no per-lane exit masks);
-            // the per-lane loop finishes the round.  NaN timing votes "short".
+            // on the likely counts let the wave run the largest count every live
+            // stream reaches as a uniform loop (no per-lane exit masks).  A stream
+            // need not finish its round: what it leaves (its backlog) stays in the
+            // ring and opens the next round, so the wave-wide count settles at
+            // the symbol rate and no per-lane remainder runs in steady state.
             {
                 const double room = static_cast<double>(rend - d - 3) - nt;
                 const double step_max = sps + 0.1;
                 const int cap_l = kmax - k;
+                // streams whose samples end in this round vote too; streams that
+                // ended earlier, stopped ones and rows past the batch do not
+                const bool live = mine && !stop && cnt > r * KB;
                 auto reaches = [&](int G) { return room >= (G - 1) * step_max && cap_l >= G; };
                 int kg = 0;
-                if (__ballot(mine && !reaches(kguar + 2)) == 0) kg = kguar + 2;
-                else if (__ballot(mine && !reaches(kguar + 1)) == 0) kg = kguar + 1;
-                else if (__ballot(mine && !reaches(kguar)) == 0) kg = kguar;
+                if (__ballot(live && !reaches(kguar + 2)) == 0) {
+                    kg = kguar + 2;
+                    if (__ballot(live && !reaches(kguar + 3)) == 0) kg = kguar + 3;
+                } else if (__ballot(live && !reaches(kguar + 1)) == 0) {
+                    kg = kguar + 1;
+                } else if (__ballot(live && !reaches(kguar)) == 0) {
+                    kg = kguar;
+                }
                 kg = __builtin_amdgcn_readfirstlane(kg);
+                kuni = kg > 0 ? kg : 0;
+                ACC(c_pre, tl);
                 STAMP(tu);
-                if (lane < SPW) {  // lanes past the batch have no row
+                if (live) {
                     // by two: the loop-carried symbol/decision registers alternate
                     // instead of being copied back every symbol
                     int u = 0;
@@ -375,9 +416,21 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                     if (u < kg) step();
                 }
                 ACC(c_uni, tu);
+#ifdef QPSK_LOOP_STAMPS
+                c_uit += kuni;
+#endif
             }
+            STAMP(tpost);
+            // per-lane catch-up: a stream's last round finishes it; before that
+            // it steps on only while it lags rend by lag_max samples or more,
+            // which bounds the backlog (ring and round capacity stay safe).
             // k < kmax also bounds a stream whose timing went NaN (base stuck)
-            while (base + 2 < rend && k < kmax) step();
+            {
+                const bool last = cnt <= (r + 1) * KB;
+                while (base + 2 < rend && k < kmax &&
+                       (last || static_cast<double>(rend - d - 3) - nt >= lag_max))
+                    step();
+            }
             if (k > 0) {
                 psi = static_cast<float>(psid);
                 psq = static_cast<float>(psqd);
@@ -400,22 +453,21 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 has_prev = 1;
                 stop = true;
             }
-            // the Costas wave runs `kfull` symbols as a uniform loop (no per-lane
-            // exit masks) and only the remainder with per-lane counts.  A round
-            // that lies inside a stream's samples holds at least
-            // floor(64 / (sps + 0.1)) symbol instants (the timing advance is at
-            // most sps + 0.1); one vote tells whether every stream reached it.
-            const bool short_round = __ballot(mine && k < kfull) != 0;
+            // the Costas wave runs the uniform count as its own uniform loop on
+            // every stream that produced at least that many symbols
             if (lane < SPW) L.cnt[(r & 3) * SPW + lane] = k;
-            if (lane == 0) L.cnt[4 * SPW + (r & 3)] = short_round ? 0 : kfull;
+            if (lane == 0) L.cnt[4 * SPW + (r & 3)] = kuni;
+            ACC(c_post, tpost);
             ACC(c_loop, tl);
         }
 #ifdef QPSK_LOOP_STAMPS
         if (a.probe && lane == 0) {
-            a.probe[blockIdx.x * 8 + 2] = c_bar;
-            a.probe[blockIdx.x * 8 + 3] = c_loop;
-            a.probe[blockIdx.x * 8 + 4] = c_iters | (c_uni << 20);
-            a.probe[blockIdx.x * 8 + 7] = NR;
+            a.probe[blockIdx.x * 16 + 2] = c_bar;
+            a.probe[blockIdx.x * 16 + 3] = c_loop;
+            a.probe[blockIdx.x * 16 + 4] = c_iters | (c_uni << 20);
+            a.probe[blockIdx.x * 16 + 7] = NR;
+            a.probe[blockIdx.x * 16 + 10] = c_uit;
+            a.probe[blockIdx.x * 16 + 11] = c_pre + (c_post << 32);
         }
 #endif
         if (!valid) return;
@@ -449,6 +501,21 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         return;
     }
 
+#ifdef QPSK_PROBE_NOCOSTAS
+    if (wave == 2) {   // diagnostic: a stand-in Costas that copies symbols through
+        for (int r = 0; r <= NR + 1; ++r) {
+            __builtin_amdgcn_s_barrier();
+            if (r == 0 || r > NR || lane >= SPW) continue;
+            const int slot = (r - 1) & 1;
+            const int m = mine ? L.cnt[((r - 1) & 3) * SPW + lane] : 0;
+            for (int k = 0; k < m; ++k) {
+                const d2 y = L.sym[(slot * SPW + lane) * L.RS + k];
+                L.rot[(slot * SPW + lane) * L.RS + k] = f2{static_cast<float>(y.x), static_cast<float>(y.y)};
+            }
+        }
+        return;
+    }
+#endif
     if (wave == 2) {
         // ============================================================ Costas
         double theta = 0.0, freq = 0.0;
@@ -460,7 +527,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         const double kTwoPi = 2.0 * 3.14159265358979311600;
         const double kPi = 3.14159265358979311600;
 #ifdef QPSK_LOOP_STAMPS
-        unsigned long long k_bar = 0, k_loop = 0;
+        unsigned long long k_bar = 0, k_loop = 0, k_uni = 0, k_uit = 0;
 #endif
         for (int r = 0; r <= NR + 1; ++r) {
             STAMP(tb);
@@ -504,11 +571,18 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             y = in[0];
             int k = 0;
             double amax = fabs(theta);   // largest sincos argument of the round
+            STAMP(tu);
+            if (m >= mlo) {              // every stream the M&M ran uniformly
 #pragma unroll 2
-            for (; k < mlo; ++k) {       // uniform trip count
-                step(k, std::false_type{});
-                amax = fmax(amax, fabs(theta));
+                for (; k < mlo; ++k) {   // uniform trip count
+                    step(k, std::false_type{});
+                    amax = fmax(amax, fabs(theta));
+                }
             }
+            ACC(k_uni, tu);
+#ifdef QPSK_LOOP_STAMPS
+            k_uit += mlo;
+#endif
             for (; k < m; ++k) {         // per-lane remainder (~1 symbol)
                 step(k, std::false_type{});
                 amax = fmax(amax, fabs(theta));
@@ -524,8 +598,10 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         }
 #ifdef QPSK_LOOP_STAMPS
         if (a.probe && lane == 0) {
-            a.probe[blockIdx.x * 8 + 5] = k_bar;
-            a.probe[blockIdx.x * 8 + 6] = k_loop;
+            a.probe[blockIdx.x * 16 + 5] = k_bar;
+            a.probe[blockIdx.x * 16 + 6] = k_loop;
+            a.probe[blockIdx.x * 16 + 8] = k_uni;
+            a.probe[blockIdx.x * 16 + 9] = k_uit;
         }
 #endif
         if (mine) {

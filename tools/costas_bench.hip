@@ -1,0 +1,207 @@
+// tools/costas_bench.hip -- cycles per symbol of the Costas step of
+// qpsk_loop.hip in isolation (one wave, LDS-resident table and symbols), with
+// variants that stub out one piece each, to see where the chain's time goes.
+// Diagnostic only; not part of the library.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <type_traits>
+
+#include "../qpsk-modulator-demodulator_amd/csrc/qpsk_sincos.h"
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+constexpr int kRS = 41, kN = 40;
+
+// V: 0 full step, 1 no wrap, 2 cheap trig (no table), 3 no amax, 4 no LDS
+// symbol read (register input), 5 no decision (pe = mq), 6 = 1+3 (no wrap/amax)
+// V >= 20: V - 20 is the Costas variant; a second wave runs an M&M-like LDS
+// pattern (two ds_read2_b64 with 4-way bank conflicts + one ds_write_b128 per
+// ~40 dependent VALU ops) for as long as the Costas wave runs
+__shared__ volatile int g_stop;
+template <int V>
+__global__ __launch_bounds__(128) void costas(const d2 *sym_g, float *out_g, long long *cyc, int reps) {
+    __shared__ double tab[1024];
+    __shared__ double tab_lo[1024];
+    __shared__ d2 sym[32 * kRS];
+    __shared__ f2 rot[32 * kRS];
+    __shared__ f2 ring[32 * 260];
+    __shared__ d2 mmout[32 * kRS];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+        tab[i] = qpsk_sincos_table_dev[i];
+        tab_lo[i] = qpsk_sincos_table_dev_lo[i];
+    }
+    for (int i = threadIdx.x; i < 32 * kRS; i += blockDim.x) sym[i] = sym_g[i];
+    for (int i = threadIdx.x; i < 32 * 260; i += blockDim.x) ring[i] = f2{0.001f * i, 0.5f};
+    if (threadIdx.x == 0) g_stop = 0;
+    __syncthreads();
+    if (wave == 1 && V >= 30 && V < 40) {      // 30: f64 VALU noise, 31: SALU noise, 32: both on 2 waves
+        double x = 1.0 + lane;
+        int sc = 0;
+        while (g_stop == 0) {
+            if (V == 30 || V == 32) {
+#pragma unroll
+                for (int j = 0; j < 32; ++j) x = fma(x, 0.9999999, 1e-9);
+            }
+            if (V == 31 || V == 32) {
+#pragma unroll
+                for (int j = 0; j < 32; ++j) asm volatile("s_add_u32 %0, %0, 1" : "+s"(sc) :: "scc");
+            }
+        }
+        out_g[64 + lane] = (float)x + sc;
+        return;
+    }
+    if (wave == 1) {
+        if (V < 20 || lane >= 32) return;
+        float acc = 0.1f * lane;
+        int idx = 5;
+        int it = 0;
+        while (g_stop == 0) {
+            const f2 *tp = ring + lane * 260 + (idx & 127);
+            const f2 a0 = tp[0], a1 = tp[1], a2 = tp[2], a3 = tp[3];
+            float v = acc + a0.x * a1.y + a2.x * a3.y;
+#pragma unroll
+            for (int j = 0; j < 36; ++j) v = v * 0.999f + 0.001f;
+            acc = v;
+            mmout[lane * kRS + (it & 31)] = d2{v, v};
+            idx += 8 + (v > 100.f);
+            ++it;
+        }
+        out_g[64 + lane] = acc;
+        return;
+    }
+    constexpr int VC = V >= 40 ? V - 40 : (V >= 30 ? 0 : (V >= 20 ? V - 20 : V));
+    if (lane >= 32) return;
+    // V 40+: the same variants with every lane's carrier phase far from the others
+    double theta = V >= 40 ? -3.0 + 0.19 * ((lane * 13) % 32) : 0.01 * lane, freq = 1e-4;
+    const double ca = 0.13751550967894244, cb = 0.010184293139132996;
+    const double kTwoPi = 2.0 * 3.14159265358979311600, kPi = 3.14159265358979311600;
+    const d2 *in = sym + lane * kRS;
+    f2 *out = rot + lane * kRS;
+    double amax = 0.0;
+    unsigned ahi = 0;
+    d2 y = in[0];
+    const d2 yreg = in[3];
+    auto step = [&](int k) {
+        const d2 yn = VC == 4 ? yreg : in[k + 1];
+        double sn, cs;
+        if (VC == 2) {
+            cs = 1.0 - 0.5 * theta * theta;
+            sn = theta;
+        } else {
+            qpsk_sincos_tab_core(theta, tab, tab_lo, &sn, &cs);
+        }
+        const double mi = y.x * cs + y.y * sn;
+        const double mq = y.y * cs - y.x * sn;
+        const float ri = static_cast<float>(mi), rq = static_cast<float>(mq);
+        double pe;
+        if (VC == 5) {
+            pe = mq - mi;
+        } else if (VC >= 7) {
+            // decision without VCC: ri + 0 turns -0 into +0 (GetSign: -0 >= 0),
+            // then the sign bit of ri goes onto 1.0 with one bitfield insert
+            const float rip = ri + 0.0f, rqp = rq + 0.0f;
+            union { double d; unsigned long long u; } ei, eq;
+            ei.u = static_cast<unsigned long long>((__float_as_uint(rip) & 0x80000000u) | 0x3ff00000u) << 32;
+            eq.u = static_cast<unsigned long long>((__float_as_uint(rqp) & 0x80000000u) | 0x3ff00000u) << 32;
+            pe = fma(ei.d, mq, -(eq.d * mi));
+        } else {
+            const double ei = ri >= 0.0f ? 1.0 : -1.0;
+            const double eq = rq >= 0.0f ? 1.0 : -1.0;
+            pe = fma(ei, mq, -(eq * mi));
+        }
+        freq = freq + cb * pe;
+        const double tn = theta + (freq + ca * pe);
+        if (VC == 1 || VC == 6 || VC == 10) {
+            theta = tn;
+        } else if (VC == 8 || VC == 9) {
+            theta = tn;
+            if (__builtin_expect(__ballot(fabs(tn) > kPi) != 0, 0)) {
+                const double tw = tn + copysign(kTwoPi, -tn);
+                theta = fabs(tn) > kPi ? tw : tn;
+            }
+        } else {
+            const double tw = tn + copysign(kTwoPi, -tn);
+            theta = fabs(tn) > kPi ? tw : tn;
+        }
+        out[k] = f2{ri, rq};
+        y = yn;
+    };
+    long long t0 = __builtin_amdgcn_s_memtime();
+    for (int r = 0; r < reps; ++r) {
+#pragma unroll 2
+        for (int k = 0; k < 8; ++k) {
+            step(k);
+            if (VC == 9 || VC == 10) {
+                union { double d; unsigned long long u; } tb;
+                tb.d = theta;
+                ahi = max(ahi, static_cast<unsigned>(tb.u >> 32) & 0x7fffffffu);
+            } else if (VC != 3 && VC != 6) {
+                amax = fmax(amax, fabs(theta));
+            }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) g_stop = 1;
+    out_g[lane] = rot[lane * kRS + 3].x + (float)theta + (float)amax + (float)ahi;
+    if (lane == 0) cyc[0] = t1 - t0;
+}
+
+template <int V>
+static void run(const char *name, const d2 *sym, float *out, long long *cyc) {
+    const int reps = 4096;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    double best = 1e30, ghz = 0;
+    for (int t = 0; t < 3; ++t) {
+        hipEventRecord(e0);
+        hipLaunchKernelGGL(costas<V>, dim3(1), dim3(128), 0, 0, sym, out, cyc, reps);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        long long c = 0;
+        hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
+        const double cy = (double)c / (reps * 8);
+        if (cy < best) { best = cy; ghz = c / (ms * 1e6); }
+    }
+    printf("%-28s %6.1f cycles/symbol (stamp rate %.2f GHz incl. launch)\n", name, best, ghz);
+}
+
+int main() {
+    d2 *sym;
+    float *out;
+    long long *cyc;
+    hipMalloc(&sym, 32 * kRS * sizeof(d2));
+    hipMalloc(&out, 128 * 4);
+    hipMalloc(&cyc, 8);
+    d2 h[32 * kRS];
+    for (int i = 0; i < 32 * kRS; ++i) h[i] = d2{0.7 * ((i * 7) % 5 - 2), 0.6 * ((i * 3) % 7 - 3)};
+    hipMemcpy(sym, h, sizeof(h), hipMemcpyHostToDevice);
+    run<0>("full step (warm-up)", sym, out, cyc);
+    run<0>("full step", sym, out, cyc);
+    run<1>("no wrap", sym, out, cyc);
+    run<2>("cheap trig (no table)", sym, out, cyc);
+    run<3>("no amax", sym, out, cyc);
+    run<4>("register input", sym, out, cyc);
+    run<5>("no decision", sym, out, cyc);
+    run<6>("no wrap, no amax", sym, out, cyc);
+    run<7>("bfi decision", sym, out, cyc);
+    run<8>("bfi decision + branch wrap", sym, out, cyc);
+    run<9>("+ integer amax", sym, out, cyc);
+    run<10>("bfi, int amax, no wrap", sym, out, cyc);
+    run<20>("full step + LDS noise wave", sym, out, cyc);
+    run<22>("cheap trig + LDS noise wave", sym, out, cyc);
+    run<30>("full + f64 VALU noise wave", sym, out, cyc);
+    run<31>("full + SALU noise wave", sym, out, cyc);
+    run<32>("full + VALU+SALU noise wave", sym, out, cyc);
+    run<40>("spread phases: full step", sym, out, cyc);
+    run<42>("spread phases: cheap trig", sym, out, cyc);
+    return 0;
+}

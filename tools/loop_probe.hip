@@ -21,8 +21,8 @@ int main(int argc, char** argv) {
   std::vector<StreamState> hs(S); for (auto& x : hs) { x = StreamState{}; x.base = 1; }
   hipMalloc(&st, S * sizeof(StreamState)); hipMemcpy(st, hs.data(), S * sizeof(StreamState), hipMemcpyHostToDevice);
   const int64_t words = n / 8;
-  hipMalloc(&bits, S * words * 4); hipMalloc(&cnt, 2 * S * 8); hipMalloc(&probe, 8 * S * 8);
-  hipMemset(probe, 0, 8 * S * 8);
+  hipMalloc(&bits, S * words * 4); hipMalloc(&cnt, 2 * S * 8); hipMalloc(&probe, 16 * S * 8);
+  hipMemset(probe, 0, 16 * S * 8);
   LoopArgs a{}; a.mf = mf; a.mf_stride = stride; a.carry = carry; a.n = n; a.state = st; a.bits = bits;
   a.bits_stride_words = words; a.bits_cap_words = words; a.n_bits = cnt; a.n_syms = cnt + S; a.S = S; a.probe = probe;
   LoopParams P{}; P.sps = 8.0; P.kp = 2.622462326512427e-3; P.ki = 3.443172085385801e-06; P.c_alpha = 0.13751550967894244; P.c_beta = 0.010184293139132996; P.differential = 1;
@@ -31,14 +31,24 @@ int main(int argc, char** argv) {
   launch_loop(a, P, kModeDemodulate, spw, 0);
   hipEventRecord(e1); hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
-  std::vector<unsigned long long> pr(8 * S); hipMemcpy(pr.data(), probe, pr.size() * 8, hipMemcpyDeviceToHost);
+  std::vector<unsigned long long> pr(16 * S); hipMemcpy(pr.data(), probe, pr.size() * 8, hipMemcpyDeviceToHost);
   int64_t ns; hipMemcpy(&ns, cnt + S, 8, hipMemcpyDeviceToHost);
   printf("S=%d n=%lld variant=%d: %.3f ms, stream0 symbols %lld -> %.1f ns/symbol\n", S, (long long)n, spw, ms, (long long)ns, ms * 1e6 / ns);
+  const int nwg = (int)((S + (spw == 0 || spw == 2 ? 32 : 16) - 1) / (spw == 0 || spw == 2 ? 32 : 16));
+  for (int b = 0; b < nwg; ++b) {
+    auto* p = &pr[16 * b];
+    printf(" WG %2d:", b);
+    for (int w = 0; w < 4; ++w) {
+      const unsigned hw = (unsigned)p[12 + w]; const unsigned xcc = (unsigned)(p[12 + w] >> 32);
+      printf(" w%d xcc%u se%u cu%2u simd%u |", w, xcc & 0xf, (hw >> 13) & 3, (hw >> 8) & 0xf, (hw >> 4) & 3);
+    }
+    printf(" M&M %.0f Costas %.0f cyc/sym\n", (double)p[3] / (p[4] & 0xfffff), (double)p[6] / (p[4] & 0xfffff));
+  }
   for (int b = 0; b < 3; ++b) {
-    auto* p = &pr[8 * b];
+    auto* p = &pr[16 * b];
     const double R = (double)p[7];
-    printf(" WG %d rounds %llu: per round cycles: loader wait %.0f bar %.0f issue %.0f | M&M bar %.0f loop %.0f | Costas bar %.0f loop %.0f | cyc/sym M&M %.0f Costas %.0f | M&M uniform-loop cycles/round %.0f\n",
-           b, p[7], p[0] / R, (p[1] & 0xffffffffull) / R, (p[1] >> 32) / R, p[2] / R, p[3] / R, p[5] / R, p[6] / R, (double)p[3] / (p[4] & 0xfffff), (double)p[6] / (p[4] & 0xfffff), (double)(p[4] >> 20) / R);
+    printf(" WG %d rounds %llu: per round cycles: loader wait %.0f bar %.0f issue %.0f | M&M bar %.0f loop %.0f | Costas bar %.0f loop %.0f | cyc/sym M&M %.0f Costas %.0f | M&M uniform-loop cycles/round %.0f (%.0f/sym) | Costas uniform %.0f/round (%.0f/sym) | M&M pre %.0f post %.0f\n",
+           b, p[7], p[0] / R, (p[1] & 0xffffffffull) / R, (p[1] >> 32) / R, p[2] / R, p[3] / R, p[5] / R, p[6] / R, (double)p[3] / (p[4] & 0xfffff), (double)p[6] / (p[4] & 0xfffff), (double)(p[4] >> 20) / R, p[10] ? (double)(p[4] >> 20) / p[10] : 0.0, p[8] / R, p[9] ? (double)p[8] / p[9] : 0.0, (p[11] & 0xffffffffull) / R, (p[11] >> 32) / R);
   }
   return 0;
 }
