@@ -182,6 +182,9 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         }
         cmin = __builtin_amdgcn_readfirstlane(cmin);
         auto issue = [&](int r) {
+#ifdef QPSK_PROBE_NOLOAD
+            return;   // diagnostic: no LDS DMA (the consumers read stale samples)
+#endif
             const int roff = (r & 3) * KB;
             if ((r + 1) * KB <= cmin) {
                 const char *rb = reinterpret_cast<const char *>(wg_mf + static_cast<int64_t>(r) * KB);
@@ -331,12 +334,21 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 cq = acc.y;
             };
             // advance timing by adv (MuellerMuller.cs:113-115) and fetch the next taps
-            auto advance = [&](double adv) {
+            // LOAD = false: a round's last uniform step fetches no taps; they
+            // would be stale (samples of the next round) and the round-start
+            // reload would first have to wait for them
+            auto advance = [&](double adv, auto load) {
                 nt = nt + adv;
                 const double fl = floor(nt);
                 mu = nt - fl;
                 base = static_cast<int>(fl) + d;
-                tp = taps_fl(fl);
+                if constexpr (decltype(load)::value) {
+                    tp = taps_fl(fl);
+                    xm1 = tp[0]; x0 = tp[1]; x1 = tp[2]; x2 = tp[3];
+                }
+            };
+            auto reload = [&]() {
+                tp = (lds_f2 *)taps(base);
                 xm1 = tp[0]; x0 = tp[1]; x1 = tp[2]; x2 = tp[3];
             };
             if (!has_prev && base + 2 < rend && kmax > 0) {
@@ -349,9 +361,9 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 psi = ci; psq = cq;
                 pdid = ci >= 0.0f ? 1.0 : -1.0;
                 pdqd = cq >= 0.0f ? 1.0 : -1.0;
-                advance(sps);
+                advance(sps, std::true_type{});
             }
-            auto step = [&]() {
+            auto step = [&](auto load) {
                 float ci, cq;
                 interp(ci, cq);
                 // M&M TED (MuellerMuller.cs:78-80)
@@ -371,7 +383,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 out[k++] = d2{cid, cqd};
                 psid = cid; psqd = cqd;
                 pdid = did; pdqd = dqd;
-                advance(sps + corr);
+                advance(sps + corr, load);
 #ifdef QPSK_LOOP_STAMPS
                 ++c_iters;
 #endif
@@ -390,15 +402,16 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const int cap_l = kmax - k;
                 // streams whose samples end in this round vote too; streams that
                 // ended earlier, stopped ones and rows past the batch do not
-                const bool live = mine && !stop && cnt > r * KB;
-                auto reaches = [&](int G) { return room >= (G - 1) * step_max && cap_l >= G; };
+                const bool live = mine & !stop & (cnt > r * KB);
+                // (bitwise & keeps each vote one compare pair, no branches)
+                auto reaches = [&](int G) { return (room >= (G - 1) * step_max) & (cap_l >= G); };
                 int kg = 0;
-                if (__ballot(live && !reaches(kguar + 2)) == 0) {
+                if (__ballot(live & !reaches(kguar + 2)) == 0) {
                     kg = kguar + 2;
-                    if (__ballot(live && !reaches(kguar + 3)) == 0) kg = kguar + 3;
-                } else if (__ballot(live && !reaches(kguar + 1)) == 0) {
+                    if (__ballot(live & !reaches(kguar + 3)) == 0) kg = kguar + 3;
+                } else if (__ballot(live & !reaches(kguar + 1)) == 0) {
                     kg = kguar + 1;
-                } else if (__ballot(live && !reaches(kguar)) == 0) {
+                } else if (__ballot(live & !reaches(kguar)) == 0) {
                     kg = kguar;
                 }
                 kg = __builtin_amdgcn_readfirstlane(kg);
@@ -409,11 +422,12 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                     // by two: the loop-carried symbol/decision registers alternate
                     // instead of being copied back every symbol
                     int u = 0;
-                    for (; u + 1 < kg; u += 2) {
-                        step();
-                        step();
+                    for (; u + 2 < kg; u += 2) {
+                        step(std::true_type{});
+                        step(std::true_type{});
                     }
-                    if (u < kg) step();
+                    if (kg - u == 2) step(std::true_type{});
+                    if (kg - u >= 1) step(std::false_type{});
                 }
                 ACC(c_uni, tu);
 #ifdef QPSK_LOOP_STAMPS
@@ -427,27 +441,27 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             // k < kmax also bounds a stream whose timing went NaN (base stuck)
             {
                 const bool last = cnt <= (r + 1) * KB;
-                while (base + 2 < rend && k < kmax &&
-                       (last || static_cast<double>(rend - d - 3) - nt >= lag_max))
-                    step();
-            }
-            if (k > 0) {
-                psi = static_cast<float>(psid);
-                psq = static_cast<float>(psqd);
+                auto more = [&]() {
+                    return (base + 2 < rend) & (k < kmax) &
+                           (last | (static_cast<double>(rend - d - 3) - nt >= lag_max));
+                };
+                if (__ballot(more()) != 0) {   // one vote skips the loop in steady state
+                    reload();                   // the uniform loop ended on a tap-less step
+                    while (more()) step(std::true_type{});
+                }
             }
             nsym += k;
-            pdi = static_cast<float>(pdid);
-            pdq = static_cast<float>(pdqd);
             if (!stop && nsym >= cap && base + 2 < rend) {
                 // MuellerMuller.cs:73-102: the symbol after the last one that fits
                 // still runs the TED/PI update, then the call stops
+                reload();
                 float ci, cq;
                 interp(ci, cq);
                 const float di = ci >= 0.0f ? 1.0f : -1.0f;
                 const float dq = cq >= 0.0f ? 1.0f : -1.0f;
-                if (has_prev) {
-                    const double t1 = static_cast<double>(pdi) * ci + static_cast<double>(pdq) * cq;
-                    const double t2 = static_cast<double>(di) * psi + static_cast<double>(dq) * psq;
+                if (has_prev) {   // psid/psqd/pdid/pdqd hold the floats exactly
+                    const double t1 = pdid * ci + pdqd * cq;
+                    const double t2 = static_cast<double>(di) * psid + static_cast<double>(dq) * psqd;
                     integ += ki * (t1 - t2);
                 }
                 has_prev = 1;
@@ -496,6 +510,11 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         g->carry_n = keep;
         g->mu = mu;
         g->integ = integ;
+        // the widened registers hold the reference's floats exactly
+        psi = static_cast<float>(psid);
+        psq = static_cast<float>(psqd);
+        pdi = static_cast<float>(pdid);
+        pdq = static_cast<float>(pdqd);
         g->psi = psi; g->psq = psq; g->pdi = pdi; g->pdq = pdq;
         g->has_prev = has_prev;
         return;
@@ -523,9 +542,16 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             theta = a.state[s].theta;
             freq = a.state[s].freq;
         }
-        const double ca = P.c_alpha, cb = P.c_beta;
-        const double kTwoPi = 2.0 * 3.14159265358979311600;
-        const double kPi = 3.14159265358979311600;
+        double ca = P.c_alpha, cb = P.c_beta;
+        double kTwoPi = 2.0 * 3.14159265358979311600;
+        double kPi = 3.14159265358979311600;
+        qpsk_sincos_consts K = QPSK_SINCOS_CONSTS_INIT;
+        // every 64-bit constant of the step lives in VGPRs for the whole wave:
+        // otherwise each iteration rebuilds some from SGPR halves (VOP3 reads
+        // one scalar operand), which costs issue slots on an issue-bound chain
+        asm volatile("" : "+v"(ca), "+v"(cb), "+v"(kTwoPi), "+v"(kPi));
+        asm volatile("" : "+v"(K.INV), "+v"(K.SH), "+v"(K.P1), "+v"(K.P2), "+v"(K.P3));
+        asm volatile("" : "+v"(K.S3), "+v"(K.S5), "+v"(K.C4), "+v"(K.C6));
 #ifdef QPSK_LOOP_STAMPS
         unsigned long long k_bar = 0, k_loop = 0, k_uni = 0, k_uit = 0;
 #endif
@@ -549,7 +575,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const d2 yn = in[k + 1];   // next symbol, read under this one's chain
                 double sn, cs;
                 if constexpr (decltype(huge)::value) qpsk_sincos_tab(theta, L.tab, L.tab_lo, &sn, &cs);
-                else qpsk_sincos_tab_core(theta, L.tab, L.tab_lo, &sn, &cs);
+                else qpsk_sincos_tab_core_k(theta, L.tab, L.tab_lo, &K, &sn, &cs);
                 const double mi = y.x * cs + y.y * sn;
                 const double mq = y.y * cs - y.x * sn;
                 const float ri = static_cast<float>(mi), rq = static_cast<float>(mq);
@@ -560,9 +586,9 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const double pe = fma(ei, mq, -(eq * mi));
                 freq = freq + cb * pe;
                 const double tn = theta + (freq + ca * pe);
-                // single +-2pi wrap (:89-91) as a select: tn + copysign(2pi, -tn)
+                // single +-2pi wrap (:89-91) as a select: tn - copysign(2pi, tn)
                 // is tn - 2pi above pi and tn + 2pi below -pi
-                const double tw = tn + copysign(kTwoPi, -tn);
+                const double tw = tn - copysign(kTwoPi, tn);
                 theta = fabs(tn) > kPi ? tw : tn;
                 out[k] = f2{ri, rq};
                 y = yn;
@@ -573,10 +599,11 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             double amax = fabs(theta);   // largest sincos argument of the round
             STAMP(tu);
             if (m >= mlo) {              // every stream the M&M ran uniformly
-#pragma unroll 2
+#pragma unroll 4
                 for (; k < mlo; ++k) {   // uniform trip count
                     step(k, std::false_type{});
-                    amax = fmax(amax, fabs(theta));
+                    // one v_max_f64 (fmax would first canonicalize amax)
+                    asm volatile("v_max_f64 %0, %0, |%1|" : "+v"(amax) : "v"(theta));
                 }
             }
             ACC(k_uni, tu);
@@ -612,6 +639,10 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     }
 
     // ================================================================ decode
+#ifdef QPSK_PROBE_NODECODE
+    for (int r = 0; r <= NR + 1; ++r) __builtin_amdgcn_s_barrier();   // diagnostic
+    return;
+#endif
     int diff_have = 0;
     float dpi = 0.f, dpq = 0.f;
     if (mine) {

@@ -46,6 +46,49 @@ QPSK_HD static inline double qpsk_sincos_arg(double x)
     return fabs(x) > 1.0e6 ? fmod(x, 6.28318530717958647693) : x;
 }
 
+/* the core's constants; a caller may hold them in registers (device loops pin
+ * them in VGPRs so no iteration rebuilds 64-bit constants) */
+typedef struct {
+    double INV, SH, P1, P2, P3, S3, S5, C4, C6;
+} qpsk_sincos_consts;
+#define QPSK_SINCOS_CONSTS_INIT                                                    \
+    {                                                                              \
+        0x1.45f306dc9c883p+6,      /* 256/pi */                                    \
+        0x1.8p+52,                 /* 1.5*2^52: ulp 1 */                           \
+        0x1.921fb54442d18p-7,      /* pi/256 rounded to double */                  \
+        0x1.1a62633145c07p-61,     /* next 53 bits */                              \
+        -0x1.f1976b7ed8fbcp-117,   /* next bits */                                 \
+        -0x1.5555555555555p-3, 0x1.1111111111111p-7,   /* -1/6, 1/120 */           \
+        0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10   /* 1/24, -1/720 */          \
+    }
+
+QPSK_HD static inline void qpsk_sincos_tab_core_k(double x, const double *tab, const double *lo,
+                                             const qpsk_sincos_consts *K, double *s, double *c)
+{
+    /* kb = x*256/pi + 1.5*2^52 rounds to an integer (ties to even), so
+     * k = kb - 1.5*2^52 = rint(x*256/pi) exactly (|x| <= 1e6) and the low
+     * mantissa bits of kb are k mod 512 in two's complement: the table index
+     * without a separate rint */
+    union { double d; unsigned long long u; } kb;
+    kb.d = x * K->INV + K->SH;
+    const double k = kb.d - K->SH;
+    double r = fma(-k, K->P1, x);                  /* Cody-Waite: |r| <= pi/512 */
+    r = fma(-k, K->P2, r);
+    r = fma(-k, K->P3, r);
+    const unsigned i = (unsigned)(kb.u & 511u) * 2u;
+    const double ts = tab[i], tc = tab[i + 1];
+    const double ls = lo[i], lc = lo[i + 1];
+    /* sin r = r + r^3(-1/6 + r^2/120), cos r - 1 = r^2(-1/2 + r^2/24 - r^4/720):
+     * truncation < 1e-19 relative for |r| <= pi/512 */
+    const double z = r * r;
+    const double r3p = (r * z) * fma(z, K->S5, K->S3);          /* sin r - r */
+    const double cm = z * fma(z, fma(z, K->C6, K->C4), -0.5);   /* cos r - 1 */
+    /* angle addition, small terms first: sin x = ts + [tc r + (tc r3p + ts cm + ls)],
+     * one significant rounding in the bracket and one in the final add: <= 1 ulp */
+    *s = ts + fma(tc, r, fma(tc, r3p, fma(ts, cm, ls)));
+    *c = tc + fma(-ts, r, fma(-ts, r3p, fma(tc, cm, lc)));
+}
+
 /* sin and cos of x, |x| <= 1e6 or NaN, given the 512-entry table (any address
  * space: the GPU kernels pass a copy staged in LDS).  Straight-line: the GPU
  * Costas loop is issue-bound and every instruction costs issue slots.  NaN
@@ -53,35 +96,8 @@ QPSK_HD static inline double qpsk_sincos_arg(double x)
 QPSK_HD static inline void qpsk_sincos_tab_core(double x, const double *tab, const double *lo,
                                            double *s, double *c)
 {
-    const double INV = 0x1.45f306dc9c883p+6;       /* 256/pi */
-    const double SH = 0x1.8p+52;                   /* 1.5*2^52: ulp 1 */
-    const double P1 = 0x1.921fb54442d18p-7;        /* pi/256 rounded to double */
-    const double P2 = 0x1.1a62633145c07p-61;       /* next 53 bits */
-    const double P3 = -0x1.f1976b7ed8fbcp-117;     /* next bits */
-    const double S3 = -0x1.5555555555555p-3, S5 = 0x1.1111111111111p-7;    /* -1/6, 1/120 */
-    const double C4 = 0x1.5555555555555p-5, C6 = -0x1.6c16c16c16c17p-10;  /* 1/24, -1/720 */
-    /* kb = x*256/pi + 1.5*2^52 rounds to an integer (ties to even), so
-     * k = kb - 1.5*2^52 = rint(x*256/pi) exactly (|x| <= 1e6) and the low
-     * mantissa bits of kb are k mod 512 in two's complement: the table index
-     * without a separate rint */
-    union { double d; unsigned long long u; } kb;
-    kb.d = x * INV + SH;
-    const double k = kb.d - SH;
-    double r = fma(-k, P1, x);                     /* Cody-Waite: |r| <= pi/512 */
-    r = fma(-k, P2, r);
-    r = fma(-k, P3, r);
-    const unsigned i = (unsigned)(kb.u & 511u) * 2u;
-    const double ts = tab[i], tc = tab[i + 1];
-    const double ls = lo[i], lc = lo[i + 1];
-    /* sin r = r + r^3(-1/6 + r^2/120), cos r - 1 = r^2(-1/2 + r^2/24 - r^4/720):
-     * truncation < 1e-19 relative for |r| <= pi/512 */
-    const double z = r * r;
-    const double r3p = (r * z) * fma(z, S5, S3);          /* sin r - r */
-    const double cm = z * fma(z, fma(z, C6, C4), -0.5);   /* cos r - 1 */
-    /* angle addition, small terms first: sin x = ts + [tc r + (tc r3p + ts cm + ls)],
-     * one significant rounding in the bracket and one in the final add: <= 1 ulp */
-    *s = ts + fma(tc, r, fma(tc, r3p, fma(ts, cm, ls)));
-    *c = tc + fma(-ts, r, fma(-ts, r3p, fma(tc, cm, lc)));
+    const qpsk_sincos_consts K = QPSK_SINCOS_CONSTS_INIT;
+    qpsk_sincos_tab_core_k(x, tab, lo, &K, s, c);
 }
 
 /* any x: the pre-reduction branch, then the table reduction */

@@ -22,7 +22,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_PKG, "_build", "libqpsk_demod.so")
+# QPSK_DEMOD_LIB points at another in-tree build of the same library (A/B
+# timing of kernel variants); it must be a libqpsk_demod.so, never a fallback
+LIB_PATH = os.environ.get("QPSK_DEMOD_LIB") or os.path.join(_PKG, "_build", "libqpsk_demod.so")
 
 QPSK_OK = 0
 QPSK_ERR_ARGUMENT = -1

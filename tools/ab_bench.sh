@@ -1,0 +1,12 @@
+#!/bin/bash
+# tools/ab_bench.sh -- alternate bench.py runs over in-tree library builds
+# (qpsk-modulator-demodulator_amd/_build/ab/lib*.so) on one box, so kernel
+# variants are compared under the same clocks.  Usage: tools/ab_bench.sh ROUNDS [bench args]
+set -e
+rounds=$1; shift
+for i in $(seq 1 "$rounds"); do
+  for lib in qpsk-modulator-demodulator_amd/_build/ab/lib*.so; do
+    out=$(QPSK_DEMOD_LIB=$PWD/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-framer --no-parity "$@")
+    echo "$(basename "$lib") $(echo "$out" | grep -o '"loop": [0-9.]*') $(echo "$out" | grep -o '"value": [0-9.]*')"
+  done
+done

@@ -21,6 +21,29 @@ constexpr int kRS = 41, kN = 40;
 // pattern (two ds_read2_b64 with 4-way bank conflicts + one ds_write_b128 per
 // ~40 dependent VALU ops) for as long as the Costas wave runs
 __shared__ volatile int g_stop;
+// candidate v2 core: kb by one fma (rint of the exact product), 2-part
+// Cody-Waite, Estrin cos polynomial; same table
+__device__ __forceinline__ void sincos_v2(double x, const double *tab, const double *lo, double *s,
+                                          double *c) {
+    const double INV = 0x1.45f306dc9c883p+6, SH = 0x1.8p+52;
+    const double P1 = 0x1.921fb54442d18p-7, P2 = 0x1.1a62633145c07p-61;
+    const double S3 = -0x1.5555555555555p-3, S5 = 0x1.1111111111111p-7;
+    const double C4 = 0x1.5555555555555p-5, C6 = -0x1.6c16c16c16c17p-10;
+    union { double d; unsigned long long u; } kb;
+    kb.d = fma(x, INV, SH);
+    const double k = kb.d - SH;
+    double r = fma(-k, P1, x);
+    r = fma(-k, P2, r);
+    const unsigned i = (unsigned)(kb.u & 511u) * 2u;
+    const double ts = tab[i], tc = tab[i + 1];
+    const double ls = lo[i], lc = lo[i + 1];
+    const double z = r * r;
+    const double r3p = (r * z) * fma(z, S5, S3);
+    const double cm = fma(z * z, fma(z, C6, C4), -0.5 * z);
+    *s = ts + fma(tc, r, fma(tc, r3p, fma(ts, cm, ls)));
+    *c = tc + fma(-ts, r, fma(-ts, r3p, fma(tc, cm, lc)));
+}
+
 template <int V>
 __global__ __launch_bounds__(128) void costas(const d2 *sym_g, float *out_g, long long *cyc, int reps) {
     __shared__ double tab[1024];
@@ -74,7 +97,7 @@ __global__ __launch_bounds__(128) void costas(const d2 *sym_g, float *out_g, lon
         out_g[64 + lane] = acc;
         return;
     }
-    constexpr int VC = V >= 40 ? V - 40 : (V >= 30 ? 0 : (V >= 20 ? V - 20 : V));
+    constexpr int VC = V >= 50 ? V : (V >= 40 ? V - 40 : (V >= 30 ? 0 : (V >= 20 ? V - 20 : V)));
     if (lane >= 32) return;
     // V 40+: the same variants with every lane's carrier phase far from the others
     double theta = V >= 40 ? -3.0 + 0.19 * ((lane * 13) % 32) : 0.01 * lane, freq = 1e-4;
@@ -84,12 +107,17 @@ __global__ __launch_bounds__(128) void costas(const d2 *sym_g, float *out_g, lon
     f2 *out = rot + lane * kRS;
     double amax = 0.0;
     unsigned ahi = 0;
+    double tnp = theta;
     d2 y = in[0];
     const d2 yreg = in[3];
     auto step = [&](int k) {
         const d2 yn = VC == 4 ? yreg : in[k + 1];
         double sn, cs;
-        if (VC == 2) {
+        if (VC == 50) {
+            sincos_v2(theta, tab, tab_lo, &sn, &cs);
+        } else if (VC == 51) {
+            sincos_v2(tnp, tab, tab_lo, &sn, &cs);
+        } else if (VC == 2) {
             cs = 1.0 - 0.5 * theta * theta;
             sn = theta;
         } else {
@@ -116,6 +144,7 @@ __global__ __launch_bounds__(128) void costas(const d2 *sym_g, float *out_g, lon
         }
         freq = freq + cb * pe;
         const double tn = theta + (freq + ca * pe);
+        tnp = tn;
         if (VC == 1 || VC == 6 || VC == 10) {
             theta = tn;
         } else if (VC == 8 || VC == 9) {
@@ -203,5 +232,7 @@ int main() {
     run<32>("full + VALU+SALU noise wave", sym, out, cyc);
     run<40>("spread phases: full step", sym, out, cyc);
     run<42>("spread phases: cheap trig", sym, out, cyc);
+    run<50>("v2 sincos core on theta", sym, out, cyc);
+    run<51>("v2 sincos core on tn (pre-wrap)", sym, out, cyc);
     return 0;
 }
