@@ -1,0 +1,335 @@
+// qpsk_fll.hip -- Band-Edge FLL (FLLBandEdgeFilter.Process, Band-Edge Filter.cs:
+// 102-129, 185-195) as a systolic 8-lane pipeline on gfx950.
+//
+// The reference band-edge dot product (ComplexDotWindow, FIRFilter.cs:144-211,
+// N = 40 taps, Vector<float>.Count = 8) sums, for output o, lane accumulator l
+// over window indices i = l + 8j (j = 0..4, window index i holds x[o-39+i]),
+// then the 8 accumulators in lane order 0..7.  Lane l's newest input for output
+// o is x[o-7+l], so the only work that waits for the newest mixed sample x[m]
+// is lane 7's last product for output m, plus the last add of the lane sum.
+// Everything else can run earlier, off the per-sample chain:
+//
+//   8 hardware lanes per stream, lane <-> reference Vector lane l.
+//   At step m lane l finishes ITS accumulator for output o = m + 7 - l: the
+//   partial sum over x[m-32], x[m-24], x[m-16], x[m-8] (computed during step
+//   m-1) plus the product with x[m].  The lane sum S_l(o) = S_{l-1}(o) + acc_l(o)
+//   arrives from lane l-1, which finished output o one step earlier: a DPP shift
+//   per step.  Lane 7 therefore holds the finished filter output for sample m.
+//
+//   Lanes of a 16-lane DPP row: two streams interleaved (even / odd lanes), so
+//   the shift is row_shr:2 and lane 0 of BOTH streams reads past the row start,
+//   which bound_ctrl turns into +0 (the reference's `accI = 0f` start; 0 + a0 ==
+//   a0 because a0, itself a sum started at +0, is never -0).
+//
+//   Lane 7 forms the band powers and the error; the error is broadcast to the
+//   stream's 8 lanes (3 DPP moves) and every lane then runs the loop filter,
+//   phase wrap, sincos and NCO mix redundantly, so every lane holds x[m+1].
+//
+//   Upper taps are the conjugates of the lower ones (Band-Edge Filter.cs:
+//   176-178), so each complex tap costs 2 packed products shared by both
+//   filters: lower = (a xr - b xi, a xi + b xr), upper = (a xr + b xi,
+//   a xi - b xr), exactly the reference's (hI*xI) - (hQ*xQ), (hI*xQ) + (hQ*xI)
+//   with hQ = -b (x - (-y) == x + y and x + (-y) == x - y in IEEE arithmetic).
+//
+// Every float op is the reference's op in the reference's order
+// (-ffp-contract=off), so the output equals the one-lane fll_kernel bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "qpsk_kernels.h"
+#include "qpsk_sincos.h"
+
+namespace qpsk {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+constexpr int kSysStreams = 32;          // streams per 256-thread block: 8 per wave
+constexpr int kRingLen = 64;             // mixed samples per stream: x[t] at t & 63 and (t & 63) + 64
+constexpr int kRingRow = 2 * kRingLen + 2;   // +2 entries: a wave's 8 rows hit distinct banks
+
+struct FllSysLds {
+    double tab[1024];                    // sincos table (qpsk_sincos.h)
+    double tab_lo[1024];
+    f2 ring[kSysStreams * kRingRow];
+    float taps[2 * kFllTaps];            // lower taps, reversed, interleaved (prologue)
+};
+
+// {x.x * v.x, x.x * v.y}
+__device__ __forceinline__ f2 mul_xlo(f2 x, f2 v) {
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "v"(x), "v"(v));
+    return r;
+}
+// {x.y * v.x, x.y * v.y}
+__device__ __forceinline__ f2 mul_xhi(f2 x, f2 v) {
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(r) : "v"(x), "v"(v));
+    return r;
+}
+// {p.x - q.y, p.y + q.x}
+__device__ __forceinline__ f2 add_swap_neglo(f2 p, f2 q) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(p), "v"(q));
+    return r;
+}
+// {p.x + q.y, p.x - q.y}
+__device__ __forceinline__ f2 add_xy_neghi(f2 p, f2 q) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(p), "v"(q));
+    return r;
+}
+// {p.y - q.x, p.y + q.x}
+__device__ __forceinline__ f2 add_yx_neglo(f2 p, f2 q) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(p), "v"(q));
+    return r;
+}
+
+template <int CTRL, int ROWM, int BANKM, bool BC>
+__device__ __forceinline__ float dpp(float old, float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                                 __builtin_bit_cast(int, v), CTRL, ROWM,
+                                                                 BANKM, BC));
+}
+// lane i <- lane i-2 of its 16-lane row; row lanes 0, 1 (reference lane 0 of
+// both streams) read +0
+__device__ __forceinline__ float shr2(float v) { return dpp<0x112, 0xf, 0xf, true>(0.0f, v); }
+// every lane <- reference lane 7 of its stream (row lane 14 for even lanes, 15
+// for odd): quad_perm [2,3,2,3] fills quad 3 with the right values, row_ror:8
+// copies quad 3 to quad 1, and a 4-lane rotate (either direction lands on
+// quad 1 or 3) fills quads 0 and 2
+__device__ __forceinline__ float bcast7(float v) {
+    const float q = dpp<0xEE, 0xf, 0xf, false>(v, v);
+    const float r = dpp<0x128, 0xf, 0x2, false>(q, q);
+    return dpp<0x124, 0xf, 0x5, false>(r, r);
+}
+
+// Band-edge products of complex tap (a, b) [packed A = {a, a}, B = {b, b}] with
+// sample x, in the layout the lane sum and the powers want:
+//   R = {upper re, lower re} = {a xr + b xi, a xr - b xi}
+//   I = {upper im, lower im} = {a xi - b xr, a xi + b xr}
+__device__ __forceinline__ void band_prod(f2 A, f2 B, f2 x, f2 &R, f2 &I) {
+    const f2 p = A * x;   // {a xr, a xi}
+    const f2 q = B * x;   // {b xr, b xi}
+    R = add_xy_neghi(p, q);
+    I = add_yx_neglo(p, q);
+}
+
+__global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
+    constexpr int N = kFllTaps;
+    static_assert(N == 40, "systolic FLL assumes 5 blocks of 8 taps");
+    __shared__ FllSysLds L;
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+        L.tab[i] = qpsk_sincos_table_dev[i];
+        L.tab_lo[i] = qpsk_sincos_table_dev_lo[i];
+    }
+    if (threadIdx.x < 2 * N) L.taps[threadIdx.x] = P.lower_rev[threadIdx.x];
+
+    const int lane = threadIdx.x & 63;
+    const int rl = lane & 15;
+    const int g = (threadIdx.x >> 4) * 2 + (rl & 1);   // stream within the block
+    const int l = rl >> 1;                               // reference Vector lane
+    const int s = blockIdx.x * kSysStreams + g;
+    const bool valid = s < a.S;
+    const int sv = valid ? s : 0;
+    const int64_t n = valid ? (a.lengths ? a.lengths[s] : a.n) : 0;
+    f2 *ring = L.ring + g * kRingRow;
+    const f2 *x = reinterpret_cast<const f2 *>(a.x) + sv * a.x_stride;
+    f2 *y = reinterpret_cast<f2 *>(a.y) + sv * a.y_stride;
+
+    StreamState *stp = a.state + sv;
+    float phase = valid ? stp->fll_phase : 0.f, freq = valid ? stp->fll_freq : 0.f;
+    const int pos0 = valid ? stp->fll_pos : 0;
+
+    // ring <- x[-39..-1] from the reference's 2N delay line: the sample written
+    // k calls to Filter ago sits at (pos - k) mod N (FIRFilter.cs:61-75)
+    const f2 *dly = reinterpret_cast<const f2 *>(a.delay) + static_cast<int64_t>(sv) * 2 * N;
+    for (int k = 1 + l; k < N; k += 8) {
+        int q = pos0 - k;
+        q += q < 0 ? N : 0;
+        const f2 v = valid ? dly[q] : f2{0.f, 0.f};
+        const int idx = (-k) & (kRingLen - 1);
+        ring[idx] = v;
+        ring[idx + kRingLen] = v;
+    }
+    __syncthreads();
+
+    // taps of this lane: reversed index l + 8j, as {a, a} and {b, b} pairs
+    f2 TA[5], TB[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const float ta = L.taps[2 * (l + 8 * j)], tb = L.taps[2 * (l + 8 * j) + 1];
+        TA[j] = f2{ta, ta};
+        TB[j] = f2{tb, tb};
+    }
+
+    // pipeline state as after step -1: lane l (< 7) holds the lane sum over
+    // lanes 0..l for output 6 - l (reference order: +0, then lanes in order)
+    f2 SR = f2{0.f, 0.f}, SI = f2{0.f, 0.f};
+    if (l < 7) {
+        for (int k = 0; k <= l; ++k) {
+            f2 ar = f2{0.f, 0.f}, ai = f2{0.f, 0.f};
+            for (int j = 0; j < 5; ++j) {
+                const float ta = L.taps[2 * (k + 8 * j)], tb = L.taps[2 * (k + 8 * j) + 1];
+                f2 R, I;
+                band_prod(f2{ta, ta}, f2{tb, tb}, ring[(-33 + 8 * j + k - l) & (kRingLen - 1)], R, I);
+                ar = ar + R;
+                ai = ai + I;
+            }
+            SR = SR + ar;
+            SI = SI + ai;
+        }
+    }
+    // partial accumulators of the step at time t (inputs x[t-32], x[t-24],
+    // x[t-16], x[t-8]); rb = ring + ((t - 32) & 63) - off, off <= 8, so the
+    // four reads are static offsets (the mirror covers the wrap)
+    f2 PR, PI;
+    auto partial = [&](const f2 *rb, int off) __attribute__((always_inline)) {
+        f2 ar = f2{0.f, 0.f}, ai = f2{0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            f2 R, I;
+            band_prod(TA[j], TB[j], rb[off + 8 * j], R, I);
+            ar = ar + R;
+            ai = ai + I;
+        }
+        PR = ar;
+        PI = ai;
+    };
+    partial(ring + ((0 - 32) & (kRingLen - 1)), 0);
+
+    const float two_pi = 2.0f * 3.14159274101257324219f;
+    const float beta = P.beta, alpha = P.alpha, fmax_ = P.max_freq, fmin_ = P.min_freq;
+    qpsk_sincos_consts K = QPSK_SINCOS_CONSTS_INIT;
+    asm volatile("" : "+v"(K.INV), "+v"(K.SH), "+v"(K.P1), "+v"(K.P2), "+v"(K.P3));
+    asm volatile("" : "+v"(K.S3), "+v"(K.S5), "+v"(K.C4), "+v"(K.C6));
+
+    // one sample (Band-Edge Filter.cs:102-129) at t = t0 + u, t0 a multiple of 8.
+    // FIRST: the call's first sample (the stored phase may be anything set_state
+    // put there).  EXACT: the IEEERemainder wrap (:185-189) behind a vote and the
+    // frequency clamp (:191-195).  Without EXACT the step tracks max |phase| and
+    // max |freq| instead, and the block is redone exactly if either left its
+    // range (the phase every ~2pi/|freq| samples, the clamp essentially never),
+    // so a block is branch-free straight-line code.
+    auto step = [&](f2 in, int64_t t0, int u, auto first, auto exact, float &amax, float &fmx)
+        __attribute__((always_inline)) {
+        float sn, cs;
+        if constexpr (decltype(first)::value) {
+            qpsk_sincosf_tab(phase, L.tab, L.tab_lo, &sn, &cs);
+        } else {
+            // |phase| <= 2pi + |freq| or NaN here: inside the table reduction's range
+            double sd, cd;
+            qpsk_sincos_tab_core_k(static_cast<double>(phase), L.tab, L.tab_lo, &K, &sd, &cd);
+            sn = static_cast<float>(sd);
+            cs = static_cast<float>(cd);
+        }
+        const f2 csn = f2{cs, sn};
+        // (inI*c - inQ*s, inI*s + inQ*c)
+        const f2 xm = add_swap_neglo(mul_xlo(in, csn), mul_xhi(in, csn));
+        f2 *wb = ring + (t0 & (kRingLen - 1));
+        wb[u] = xm;
+        wb[u + kRingLen] = xm;
+        y[t0 + u] = xm;
+        f2 R4, I4;
+        band_prod(TA[4], TB[4], xm, R4, I4);
+        const f2 ar = PR + R4, ai = PI + I4;
+        SR = f2{shr2(SR.x) + ar.x, shr2(SR.y) + ar.y};
+        SI = f2{shr2(SI.x) + ai.x, shr2(SI.y) + ai.y};
+        // lane 7 holds the filter outputs of sample t: {pow upper, pow lower}
+        const f2 pw = SR * SR + SI * SI;
+        const float err = bcast7(pw.y - pw.x);
+        freq = freq + beta * err;
+        phase = phase + (freq + alpha * err);
+        if constexpr (decltype(exact)::value) {
+            if (__builtin_expect(__ballot(fabsf(phase) > two_pi) != 0, 0))
+                if (fabsf(phase) > two_pi) phase = remainderf(phase, two_pi);
+            freq = freq > fmax_ ? fmax_ : (freq < fmin_ ? fmin_ : freq);
+        } else {
+            amax = fmaxf(amax, fabsf(phase));   // NaN never wraps or clamps: ignored
+            fmx = fmaxf(fmx, fabsf(freq));
+        }
+        partial(ring + ((t0 - 32) & (kRingLen - 1)), u + 1);
+    };
+    // 8 samples of every stream of the wave, no masks
+    auto block = [&](const f2 *in, int64_t t0, auto first) __attribute__((always_inline)) {
+        const float ph0 = phase, fr0 = freq;
+        const f2 sr0 = SR, si0 = SI, pr0 = PR, pi0 = PI;
+        float amax = 0.f, fmx = 0.f;
+        step(in[0], t0, 0, first, std::false_type{}, amax, fmx);
+#pragma unroll
+        for (int u = 1; u < 8; ++u) step(in[u], t0, u, std::false_type{}, std::false_type{}, amax, fmx);
+        if (__builtin_expect(__ballot((amax > two_pi) | (fmx > fmax_)) != 0, 0)) {
+            // some stream's phase needed a wrap or its frequency a clamp: redo
+            // from the block start (its ring slots and outputs are rewritten)
+            phase = ph0; freq = fr0; SR = sr0; SI = si0; PR = pr0; PI = pi0;
+            step(in[0], t0, 0, first, std::true_type{}, amax, fmx);
+#pragma unroll
+            for (int u = 1; u < 8; ++u) step(in[u], t0, u, std::false_type{}, std::true_type{}, amax, fmx);
+        }
+    };
+
+    // wave-uniform block counts (8 streams per wave); rows past the batch count
+    // as empty streams, so only full waves take the unmasked path
+    int64_t nmax = n, nmin = n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t w1 = __shfl_xor(nmax, o, 64), w2 = __shfl_xor(nmin, o, 64);
+        nmax = w1 > nmax ? w1 : nmax;
+        nmin = w2 < nmin ? w2 : nmin;
+    }
+    // input: every lane of a stream loads the stream's next 8 samples (one
+    // block ahead); the loads of a block are the same addresses for 8 lanes
+    f2 cur[8], nxt[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) nxt[u] = u < n ? x[u] : f2{0.f, 0.f};
+    for (int64_t t0 = 0; t0 < nmax; t0 += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
+        if (t0 + 16 <= nmin) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) nxt[u] = x[t0 + 8 + u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) nxt[u] = t0 + 8 + u < n ? x[t0 + 8 + u] : f2{0.f, 0.f};
+        }
+        if (t0 + 8 <= nmin) {
+            if (t0 == 0) block(cur, t0, std::true_type{});
+            else block(cur, t0, std::false_type{});
+        } else {
+            float amax = 0.f, fmx = 0.f;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (t0 + u < n) {
+                    if (t0 + u == 0) step(cur[u], t0, u, std::true_type{}, std::true_type{}, amax, fmx);
+                    else step(cur[u], t0, u, std::false_type{}, std::true_type{}, amax, fmx);
+                }
+        }
+    }
+
+    if (n > 0) {
+        // the 2N delay line as the reference leaves it: position q holds the
+        // newest sample written there, x[n-1 - ((pos_end - 1 - q) mod N)]
+        const int pos_end = static_cast<int>((pos0 + n) % N);
+        f2 *dw = reinterpret_cast<f2 *>(a.delay) + static_cast<int64_t>(s) * 2 * N;
+        for (int q = l; q < N; q += 8) {
+            int back = pos_end - 1 - q;
+            back += back < 0 ? N : 0;
+            const f2 v = ring[(n - 1 - back) & (kRingLen - 1)];
+            dw[q] = v;
+            dw[q + N] = v;
+        }
+        if (l == 0) {
+            stp->fll_phase = phase;
+            stp->fll_freq = freq;
+            stp->fll_pos = pos_end;
+        }
+    }
+}
+
+void launch_fll_sys(const FllArgs &a, const FllParams &P, hipStream_t stream) {
+    hipLaunchKernelGGL(fll_sys_kernel, dim3((a.S + kSysStreams - 1) / kSysStreams), dim3(256), 0, stream, a,
+                       P);
+}
+
+}  // namespace qpsk

@@ -65,5 +65,6 @@ void launch_fir_hist(const FirArgs &a, float *hist_new, int H, int S, hipStream_
 void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant,
                  hipStream_t stream);
 void launch_fll(const FllArgs &a, const FllParams &P, hipStream_t stream);
+void launch_fll_sys(const FllArgs &a, const FllParams &P, hipStream_t stream);   // qpsk_fll.hip
 
 }  // namespace qpsk

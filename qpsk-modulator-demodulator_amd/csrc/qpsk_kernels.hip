@@ -515,6 +515,10 @@ void launch_fir_hist(const FirArgs &a, float *hist_new, int H, int S, hipStream_
 
 
 void launch_fll(const FllArgs &a, const FllParams &P, hipStream_t stream) {
+    if (P.lanes == 8 && kFllTaps == 40 && P.conj_taps) {
+        launch_fll_sys(a, P, stream);
+        return;
+    }
     if (P.lanes == 8 && kFllTaps % 8 == 0) {
         hipLaunchKernelGGL(fll8_kernel, dim3((a.S + kFll8Streams - 1) / kFll8Streams), dim3(256), 0,
                            stream, a, P);

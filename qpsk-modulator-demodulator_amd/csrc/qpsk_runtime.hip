@@ -180,6 +180,15 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
         h->fp.upper_rev[2 * k] = h->d.fll_upper_iq[2 * src];
         h->fp.upper_rev[2 * k + 1] = h->d.fll_upper_iq[2 * src + 1];
     }
+    // the systolic FLL shares the products of both band-edge filters, which needs
+    // upper = conj(lower) exactly (Band-Edge Filter.cs:176-178 builds it so)
+    h->fp.conj_taps = 1;
+    for (int k = 0; k < 2 * kFllTaps; ++k) {
+        uint32_t lo, up;
+        std::memcpy(&lo, &h->fp.lower_rev[k], 4);
+        std::memcpy(&up, &h->fp.upper_rev[k], 4);
+        if (up != ((k & 1) ? (lo ^ 0x80000000u) : lo)) h->fp.conj_taps = 0;
+    }
 
     auto cleanup_fail = [&](int code) {
         qpsk_demod_destroy(h);

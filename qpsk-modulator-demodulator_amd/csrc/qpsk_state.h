@@ -48,6 +48,7 @@ struct FllParams {
     float lower_rev[2 * kFllTaps]; // interleaved complex taps, reversed
     float upper_rev[2 * kFllTaps]; // (ComplexFIRFilter ctor, FIRFilter.cs:43-48)
     int32_t lanes;
+    int32_t conj_taps;             // upper_rev == conj(lower_rev) bit for bit (the reference design)
 };
 
 }  // namespace qpsk

@@ -163,6 +163,25 @@ def test_fll_mode_bit_exact():
                 oracle_run(iq, calls, 8, 8, enable_fll=True, cfo_loop_bw=1e-3))
 
 
+def test_fll_ragged_chunks_bit_exact():
+    """Systolic FLL (qpsk_fll.hip): ragged per-stream call lengths, calls shorter
+    than one 8-sample block and than the 40-tap window, empty calls, and a
+    batch that leaves most rows of the last workgroup empty."""
+    S = 11
+    iq = K.batch_signals(S, seed0=95, sps=8, span=8, n_bits=900, cfo_hz=-3000.0, snr_db=22)
+    n = iq.shape[1] // 2
+    rng = np.random.default_rng(7)
+    calls, used = [], np.zeros(S, np.int64)
+    for c in range(8):
+        lens = rng.integers(0, 50, S) if c < 6 else np.full(S, 37)
+        lens[c % S] = 0
+        calls.append([int(v) for v in lens])
+        used += lens
+    calls.append([int(n - u) for u in used])
+    assert_same(gpu_run(iq, calls, 8, 8, enable_fll=True, cfo_loop_bandwidth=1e-3),
+                oracle_run(iq, calls, 8, 8, enable_fll=True, cfo_loop_bw=1e-3))
+
+
 def test_state_checkpoint_roundtrip():
     iq = K.batch_signals(2, seed0=100, n_bits=1600, snr_db=15)
     n = iq.shape[1] // 2
