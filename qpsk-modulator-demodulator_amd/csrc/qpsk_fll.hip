@@ -40,6 +40,11 @@
 #include "qpsk_kernels.h"
 #include "qpsk_sincos.h"
 
+#ifndef QPSK_FLL_PROBE
+#define QPSK_FLL_PROBE 0   // diagnostic bits (timing only, results wrong): 1 no sincos, 2 no
+                           // partial sums, 4 no broadcast, 8 no redo; 0 = product
+#endif
+
 namespace qpsk {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -134,7 +139,12 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
     const bool valid = s < a.S;
     const int sv = valid ? s : 0;
     const int64_t n = valid ? (a.lengths ? a.lengths[s] : a.n) : 0;
-    f2 *ring = L.ring + g * kRingRow;
+    // the row's LDS address lives in one VGPR (opaque), so every ring access is
+    // that register plus a small immediate: pairs merge into ds_read2/ds_write2
+    typedef __attribute__((address_space(3))) f2 lds_f2;
+    uint32_t ring_addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_f2 *)(L.ring + g * kRingRow)));
+    asm volatile("" : "+v"(ring_addr));
+    lds_f2 *ring = reinterpret_cast<lds_f2 *>(static_cast<uintptr_t>(ring_addr));
     const f2 *x = reinterpret_cast<const f2 *>(a.x) + sv * a.x_stride;
     f2 *y = reinterpret_cast<f2 *>(a.y) + sv * a.y_stride;
 
@@ -185,10 +195,14 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
     // x[t-16], x[t-8]); rb = ring + ((t - 32) & 63) - off, off <= 8, so the
     // four reads are static offsets (the mirror covers the wrap)
     f2 PR, PI;
-    auto partial = [&](const f2 *rb, int off) __attribute__((always_inline)) {
-        f2 ar = f2{0.f, 0.f}, ai = f2{0.f, 0.f};
+    auto partial = [&](const lds_f2 *rb, int off) __attribute__((always_inline)) {
+        // the reference starts each lane accumulator at +0 (Vector<float>.Zero);
+        // 0 + v differs from v only in the sign of a zero, and the filter
+        // outputs are only ever squared (the band powers), so the start is dropped
+        f2 ar, ai;
+        band_prod(TA[0], TB[0], rb[off], ar, ai);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 1; j < 4; ++j) {
             f2 R, I;
             band_prod(TA[j], TB[j], rb[off + 8 * j], R, I);
             ar = ar + R;
@@ -217,28 +231,40 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
         float sn, cs;
         if constexpr (decltype(first)::value) {
             qpsk_sincosf_tab(phase, L.tab, L.tab_lo, &sn, &cs);
+#if QPSK_FLL_PROBE & 1
+        } else if (true) {   // diagnostic: no sincos on the chain
+            sn = phase * 0.5f;
+            cs = 1.0f - phase;
+#endif
         } else {
-            // |phase| <= 2pi + |freq| or NaN here: inside the table reduction's range
+            // a kept result has |phase| <= 2pi (or NaN): the float-argument core
             double sd, cd;
-            qpsk_sincos_tab_core_k(static_cast<double>(phase), L.tab, L.tab_lo, &K, &sd, &cd);
+            qpsk_sincos_tab_core_f(static_cast<double>(phase), L.tab, L.tab_lo, &K, &sd, &cd);
             sn = static_cast<float>(sd);
             cs = static_cast<float>(cd);
         }
         const f2 csn = f2{cs, sn};
         // (inI*c - inQ*s, inI*s + inQ*c)
         const f2 xm = add_swap_neglo(mul_xlo(in, csn), mul_xhi(in, csn));
-        f2 *wb = ring + (t0 & (kRingLen - 1));
+        lds_f2 *wb = ring + (t0 & (kRingLen - 1));
         wb[u] = xm;
         wb[u + kRingLen] = xm;
         y[t0 + u] = xm;
         f2 R4, I4;
         band_prod(TA[4], TB[4], xm, R4, I4);
+#if QPSK_FLL_PROBE & 2
+        PR = f2{0.f, 0.f}; PI = f2{0.f, 0.f};   // diagnostic: no partial-sum work
+#endif
         const f2 ar = PR + R4, ai = PI + I4;
         SR = f2{shr2(SR.x) + ar.x, shr2(SR.y) + ar.y};
         SI = f2{shr2(SI.x) + ai.x, shr2(SI.y) + ai.y};
         // lane 7 holds the filter outputs of sample t: {pow upper, pow lower}
         const f2 pw = SR * SR + SI * SI;
+#if QPSK_FLL_PROBE & 4
+        const float err = pw.y - pw.x;   // diagnostic: no broadcast
+#else
         const float err = bcast7(pw.y - pw.x);
+#endif
         freq = freq + beta * err;
         phase = phase + (freq + alpha * err);
         if constexpr (decltype(exact)::value) {
@@ -249,7 +275,9 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
             amax = fmaxf(amax, fabsf(phase));   // NaN never wraps or clamps: ignored
             fmx = fmaxf(fmx, fabsf(freq));
         }
+#if !(QPSK_FLL_PROBE & 2)
         partial(ring + ((t0 - 32) & (kRingLen - 1)), u + 1);
+#endif
     };
     // 8 samples of every stream of the wave, no masks
     auto block = [&](const f2 *in, int64_t t0, auto first) __attribute__((always_inline)) {
@@ -259,7 +287,7 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
         step(in[0], t0, 0, first, std::false_type{}, amax, fmx);
 #pragma unroll
         for (int u = 1; u < 8; ++u) step(in[u], t0, u, std::false_type{}, std::false_type{}, amax, fmx);
-        if (__builtin_expect(__ballot((amax > two_pi) | (fmx > fmax_)) != 0, 0)) {
+        if (!(QPSK_FLL_PROBE & 8) && __builtin_expect(__ballot((amax > two_pi) | (fmx > fmax_)) != 0, 0)) {
             // some stream's phase needed a wrap or its frequency a clamp: redo
             // from the block start (its ring slots and outputs are rewritten)
             phase = ph0; freq = fr0; SR = sr0; SI = si0; PR = pr0; PI = pi0;
@@ -278,21 +306,45 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
         nmax = w1 > nmax ? w1 : nmax;
         nmin = w2 < nmin ? w2 : nmin;
     }
-    // input: every lane of a stream loads the stream's next 8 samples (one
-    // block ahead); the loads of a block are the same addresses for 8 lanes
-    f2 cur[8], nxt[8];
+    // Input: every lane of a stream loads the stream's 8 samples of a block
+    // (the same addresses for its 8 lanes).  Full double blocks run from two
+    // register buffers A and B, each reloaded right after its block, so a
+    // buffer's loads have a whole block to land and nothing is copied; the
+    // only vector-memory traffic between them is the previous block's y stores,
+    // and the wait before a block's first use covers just its own loads.
+    auto load8 = [&](f2 *buf, int64_t t0) __attribute__((always_inline)) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) nxt[u] = u < n ? x[u] : f2{0.f, 0.f};
-    for (int64_t t0 = 0; t0 < nmax; t0 += 8) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
-        if (t0 + 16 <= nmin) {
-#pragma unroll
-            for (int u = 0; u < 8; ++u) nxt[u] = x[t0 + 8 + u];
+        for (int u = 0; u < 8; ++u) buf[u] = x[t0 + u];
+    };
+    int64_t t0 = 0;
+    if (nmin >= 16) {
+        f2 A[8], B[8];
+        load8(A, 0);
+        load8(B, 8);
+        if (nmin >= 32) {
+            block(A, 0, std::true_type{});
+            load8(A, 16);
+            block(B, 8, std::false_type{});
+            load8(B, 24);
+            for (t0 = 16; t0 + 32 <= nmin; t0 += 16) {
+                block(A, t0, std::false_type{});
+                load8(A, t0 + 16);
+                block(B, t0 + 8, std::false_type{});
+                load8(B, t0 + 24);
+            }
+            block(A, t0, std::false_type{});
+            block(B, t0 + 8, std::false_type{});
         } else {
-#pragma unroll
-            for (int u = 0; u < 8; ++u) nxt[u] = t0 + 8 + u < n ? x[t0 + 8 + u] : f2{0.f, 0.f};
+            block(A, 0, std::true_type{});
+            block(B, 8, std::false_type{});
         }
+        t0 += 16;
+    }
+    // the rest (ragged streams, short calls, partly filled waves), block by block
+    for (; t0 < nmax; t0 += 8) {
+        f2 cur[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) cur[u] = t0 + u < n ? x[t0 + u] : f2{0.f, 0.f};
         if (t0 + 8 <= nmin) {
             if (t0 == 0) block(cur, t0, std::true_type{});
             else block(cur, t0, std::false_type{});

@@ -13,7 +13,8 @@
 //                      decision, differential decode and MSB-first bit packing
 //                      (QPSKDeModulator.cs:372-408); one lane per stream.
 //   fll_kernel         FLLBandEdgeFilter.Process (Band-Edge Filter.cs:64-129),
-//                      one lane per stream.
+//                      one lane per stream (any Vector width); the 8-lane
+//                      systolic kernel is in qpsk_fll.hip.
 //
 // Compiled with -ffp-contract=off: every float/double op rounds exactly as the
 // reference C# (which never fuses a*b+c).  The only fma() calls are the explicit
@@ -302,168 +303,6 @@ __global__ __launch_bounds__(64) void fll_kernel(FllArgs a, FllParams P) {
 }
 
 // ---------------------------------------------------------------------------
-// Band-Edge FLL, 8 lanes per stream (Vector<float>.Count = 8 only)
-// ---------------------------------------------------------------------------
-// The reference's 40-tap band-edge dot product (FIRFilter.cs:144-211) sums
-// lane accumulator l over window indices l, l+8, ..., l+32 and then the 8
-// accumulators in order.  Here lane l of an 8-lane group IS accumulator l of
-// both filters, so each lane does 5 complex MACs per filter per sample instead
-// of 40, and a wave carries 8 streams (1024 waves at S = 8192).  The serial
-// per-sample part (sincos, mix, loop filter) is computed redundantly by the
-// 8 lanes of a group.  Window: a per-stream 2N ring in LDS (written once per
-// sample, read 5 times per lane), the newest sample taken from registers.
-// Accumulators are summed in order after an LDS transpose.  Same IEEE ops in
-// the same order as fll_kernel, so bit-identical.
-constexpr int kFll8Streams = 32;   // streams per 256-thread block
-
-// (a.x - b.x, a.y + b.y) in one v_pk_add_f32 (hipcc otherwise negates one lane
-// with a separate op and re-pairs the halves with v_mov)
-__device__ __forceinline__ f2 pk_sub_add(f2 a, f2 b) {
-    f2 r;
-    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-
-__global__ __launch_bounds__(256) void fll8_kernel(FllArgs a, FllParams P) {
-    constexpr int N = kFllTaps;              // 40 = 5 blocks of 8
-    constexpr int J = N / 8;
-    __shared__ double tab[1024];
-    __shared__ double tab_lo[1024];
-    __shared__ f2 ring[kFll8Streams][2 * N];
-    __shared__ float4 accs[kFll8Streams][8];  // (up I, up Q, lo I, lo Q) per lane accumulator
-    __shared__ f2 stage[kFll8Streams][8];     // this block of 8 input samples per stream
-    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
-        tab[i] = qpsk_sincos_table_dev[i];
-        tab_lo[i] = qpsk_sincos_table_dev_lo[i];
-    }
-    const int g = threadIdx.x >> 3;          // stream within the block
-    const int l = threadIdx.x & 7;           // lane accumulator
-    const int s = blockIdx.x * kFll8Streams + g;
-    const bool valid = s < a.S;
-    const int64_t n = valid ? (a.lengths ? a.lengths[s] : a.n) : 0;
-    const f2 *dly = reinterpret_cast<const f2 *>(a.delay) + static_cast<int64_t>(valid ? s : 0) * 2 * N;
-    for (int i = l; i < 2 * N; i += 8) ring[g][i] = valid ? dly[i] : f2{0.f, 0.f};
-    // taps of accumulator l: index l + 8j (reversed taps, as fll_dot)
-    float uhi[J], uhq[J], lhi[J], lhq[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        uhi[j] = P.upper_rev[2 * (l + 8 * j)];
-        uhq[j] = P.upper_rev[2 * (l + 8 * j) + 1];
-        lhi[j] = P.lower_rev[2 * (l + 8 * j)];
-        lhq[j] = P.lower_rev[2 * (l + 8 * j) + 1];
-    }
-    __syncthreads();
-    StreamState st;
-    if (valid) st = a.state[s];
-    float phase = valid ? st.fll_phase : 0.f, freq = valid ? st.fll_freq : 0.f;
-    int pos = valid ? st.fll_pos : 0;
-    const float two_pi = 2.0f * 3.14159274101257324219f;
-    const f2 *x = reinterpret_cast<const f2 *>(a.x) + (valid ? s : 0) * a.x_stride;
-    f2 *y = reinterpret_cast<f2 *>(a.y) + (valid ? s : 0) * a.y_stride;
-    // wave-uniform trip counts (8 streams per wave): blocks below the shortest
-    // stream run without per-sample masks, the rest masks ragged groups
-    int64_t nmax = n, nmin = valid ? n : INT64_MAX;
-#pragma unroll
-    for (int o = 8; o < 64; o <<= 1) {
-        const int64_t w1 = __shfl_xor(nmax, o, 64), w2 = __shfl_xor(nmin, o, 64);
-        nmax = w1 > nmax ? w1 : nmax;
-        nmin = w2 < nmin ? w2 : nmin;
-    }
-    // one sample of one stream (Band-Edge Filter.cs:102-129), bit-identical to fll_kernel
-    auto sample = [&](int k, int64_t t, bool first) {
-        // older window samples (indices l + 8j <= 38 were written before this
-        // sample); index 39 (j = 4, l = 7) is this sample's mix, below
-        int start = pos + 1;
-        if (start >= N) start -= N;
-        f2 w[J];
-#pragma unroll
-        for (int j = 0; j < J; ++j) w[j] = ring[g][start + l + 8 * j];
-        const f2 in = stage[g][k];
-        float sn, cs;
-        // After a sample the phase is wrapped into [-2pi, 2pi] (or NaN), so only
-        // a call's first sample, with the stored phase, can need the |x| > 1e6
-        // pre-reduction; later samples use the table core directly.
-        if (first) qpsk_sincosf_tab(phase, tab, tab_lo, &sn, &cs);
-        else {
-            double sd, cd;
-            qpsk_sincos_tab_core(static_cast<double>(phase), tab, tab_lo, &sd, &cd);
-            sn = static_cast<float>(sd);
-            cs = static_cast<float>(cd);
-        }
-        const float oi = in.x * cs - in.y * sn;
-        const float oq = in.x * sn + in.y * cs;
-        const f2 o = f2{oi, oq};
-        // every lane of the group stores the same value (no lane mask)
-        y[t] = o;
-        ring[g][pos] = o;
-        ring[g][pos + N] = o;
-        w[J - 1] = l == 7 ? o : w[J - 1];
-        // lane accumulator l of both filters (fll_dot, W = 8), I and Q packed:
-        // (hi*xr - hq*xi, hi*xi + hq*xr) = hi*(xr, xi) + (-(hq*xi), hq*xr)
-        f2 ua = f2{0.f, 0.f}, la = f2{0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const f2 ws = f2{w[j].y, w[j].x};
-            const f2 ub = uhq[j] * ws, lb = lhq[j] * ws;
-            ua = ua + pk_sub_add(uhi[j] * w[j], ub);
-            la = la + pk_sub_add(lhi[j] * w[j], lb);
-        }
-        accs[g][l] = make_float4(ua.x, ua.y, la.x, la.y);
-        asm volatile("" ::: "memory");   // group lanes write, then read each other's
-        f2 up = f2{0.f, 0.f}, lo = f2{0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {      // horizontal sum in lane order (:176-180)
-            const float4 v = accs[g][q];
-            up = up + f2{v.x, v.y};
-            lo = lo + f2{v.z, v.w};
-        }
-        asm volatile("" ::: "memory");
-        const float pu = up.x * up.x + up.y * up.y;
-        const float pl = lo.x * lo.x + lo.y * lo.y;
-        const float err = pl - pu;
-        freq += P.beta * err;
-        phase += freq + P.alpha * err;
-        // IEEERemainder wrap (:185-189), rare: one vote keeps it off the common path
-        if (__builtin_expect(__ballot(fabsf(phase) > two_pi) != 0, 0))
-            if (fabsf(phase) > two_pi) phase = remainderf(phase, two_pi);
-        freq = freq > P.max_freq ? P.max_freq : (freq < P.min_freq ? P.min_freq : freq);
-        ++pos;
-        pos = pos == N ? 0 : pos;
-    };
-    // input in blocks of 8 samples: lane l loads sample t0 + l of its stream
-    // one block ahead, the block is staged in LDS and broadcast per sample
-    f2 pre = l < n ? x[l] : f2{0.f, 0.f};
-    for (int64_t t0 = 0; t0 < nmax; t0 += 8) {
-        stage[g][l] = pre;
-        pre = t0 + 8 + l < n ? x[t0 + 8 + l] : f2{0.f, 0.f};
-        asm volatile("" ::: "memory");
-        if (t0 + 8 <= nmin) {
-            if (valid) {   // groups past the batch alias stream 0's rows: keep them out
-                if (t0 == 0) sample(0, 0, true);
-                else sample(0, t0, false);
-#pragma unroll
-                for (int k = 1; k < 8; ++k) sample(k, t0 + k, false);
-            }
-        } else {
-            for (int k = 0; k < 8; ++k)
-                if (t0 + k < n) sample(k, t0 + k, t0 + k == 0);
-        }
-        asm volatile("" ::: "memory");
-    }
-    __syncthreads();
-    if (valid && n > 0) {
-        f2 *dw = reinterpret_cast<f2 *>(a.delay) + static_cast<int64_t>(s) * 2 * N;
-        for (int i = l; i < 2 * N; i += 8) dw[i] = ring[g][i];
-        if (l == 0) {
-            st.fll_phase = phase;
-            st.fll_freq = freq;
-            st.fll_pos = pos;
-            a.state[s] = st;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
 template <int T>
@@ -515,13 +354,10 @@ void launch_fir_hist(const FirArgs &a, float *hist_new, int H, int S, hipStream_
 
 
 void launch_fll(const FllArgs &a, const FllParams &P, hipStream_t stream) {
+    // the systolic 8-lane kernel (qpsk_fll.hip) for the reference's Vector<float>
+    // width 8 and conjugate band-edge taps; the one-lane kernel otherwise
     if (P.lanes == 8 && kFllTaps == 40 && P.conj_taps) {
         launch_fll_sys(a, P, stream);
-        return;
-    }
-    if (P.lanes == 8 && kFllTaps % 8 == 0) {
-        hipLaunchKernelGGL(fll8_kernel, dim3((a.S + kFll8Streams - 1) / kFll8Streams), dim3(256), 0,
-                           stream, a, P);
         return;
     }
     const int threads = 64;

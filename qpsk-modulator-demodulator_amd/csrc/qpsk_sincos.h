@@ -89,6 +89,31 @@ QPSK_HD static inline void qpsk_sincos_tab_core_k(double x, const double *tab, c
     *c = tc + fma(-ts, r, fma(-ts, r3p, fma(tc, cm, lc)));
 }
 
+/* The same core for a FLOAT argument |x| <= 2pi (the FLL phase after its
+ * wrap), two f64 ops shorter: kb from one fma and no k*P3 term.  For every such
+ * float it returns the same doubles as qpsk_sincos_tab_core_k, checked
+ * exhaustively over all 2.17e9 of them (tools/check_sincosf_core.c; a strided
+ * subset runs in tests/test_oracle.py).  Why: x - k*P1 is exact for a float x,
+ * |r| stays far above 2^-60, so k*P3 (< 2^-106) is below half an ulp of r, and
+ * the fused x*INV + SH rounds to the same integer k. */
+QPSK_HD static inline void qpsk_sincos_tab_core_f(double x, const double *tab, const double *lo,
+                                             const qpsk_sincos_consts *K, double *s, double *c)
+{
+    union { double d; unsigned long long u; } kb;
+    kb.d = fma(x, K->INV, K->SH);
+    const double k = kb.d - K->SH;
+    double r = fma(-k, K->P1, x);
+    r = fma(-k, K->P2, r);
+    const unsigned i = (unsigned)(kb.u & 511u) * 2u;
+    const double ts = tab[i], tc = tab[i + 1];
+    const double ls = lo[i], lc = lo[i + 1];
+    const double z = r * r;
+    const double r3p = (r * z) * fma(z, K->S5, K->S3);
+    const double cm = z * fma(z, fma(z, K->C6, K->C4), -0.5);
+    *s = ts + fma(tc, r, fma(tc, r3p, fma(ts, cm, ls)));
+    *c = tc + fma(-ts, r, fma(-ts, r3p, fma(tc, cm, lc)));
+}
+
 /* sin and cos of x, |x| <= 1e6 or NaN, given the 512-entry table (any address
  * space: the GPU kernels pass a copy staged in LDS).  Straight-line: the GPU
  * Costas loop is issue-bound and every instruction costs issue slots.  NaN

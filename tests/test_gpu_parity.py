@@ -155,12 +155,14 @@ def test_libm_oracle_bits_equal_symbols_close():
     assert_same(gpu_run(iq, calls, 8, 8), oracle_run(iq, calls, 8, 8, trig=O.TRIG_LIBM), exact=False)
 
 
-def test_fll_mode_bit_exact():
+@pytest.mark.parametrize("lanes", [8, 4])
+def test_fll_mode_bit_exact(lanes):
+    """lanes 8: the systolic FLL kernel; other widths: the one-lane kernel."""
     iq = K.batch_signals(3, seed0=90, sps=8, span=8, n_bits=1200, cfo_hz=4000.0, snr_db=25)
     n = iq.shape[1] // 2
     calls = [[n // 2] * 3, [n - n // 2] * 3]
-    assert_same(gpu_run(iq, calls, 8, 8, enable_fll=True, cfo_loop_bandwidth=1e-3),
-                oracle_run(iq, calls, 8, 8, enable_fll=True, cfo_loop_bw=1e-3))
+    assert_same(gpu_run(iq, calls, 8, 8, enable_fll=True, cfo_loop_bandwidth=1e-3, vector_lanes=lanes),
+                oracle_run(iq, calls, 8, 8, enable_fll=True, cfo_loop_bw=1e-3, lanes=lanes))
 
 
 def test_fll_ragged_chunks_bit_exact():

@@ -9,6 +9,7 @@ restatement as far as the repository allows:
     holds for the oracle.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -144,3 +145,17 @@ def test_fll_ctor_validation():
         O.OracleDemod(K.FS, K.FS // 8, 1.5, 8)         # rolloff > 1
     with pytest.raises(ValueError):
         O.OracleDemod(K.FS, K.FS // 8, 0.4, 8, cfo_loop_bw=-1.0)
+
+
+def test_float_argument_sincos_core_equals_full_core(tmp_path):
+    """qpsk_sincos_tab_core_f (FLL fast path) == qpsk_sincos_tab_core for float
+    |x| <= 2pi.  Every 61st float here; tools/check_sincosf_core.c with stride 1
+    covers all 2.17e9 (FLL)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "check_sincosf")
+    subprocess.check_call(["gcc", "-O2", "-fopenmp", "-ffp-contract=off",
+                           "-I" + os.path.join(root, "qpsk-modulator-demodulator_amd", "csrc"),
+                           "-o", exe, os.path.join(root, "tools", "check_sincosf_core.c"), "-lm"])
+    out = subprocess.run([exe, "61"], capture_output=True, text=True, check=True).stdout
+    assert out.strip().endswith(" 0 differ"), out

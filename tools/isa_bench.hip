@@ -16,6 +16,8 @@ __global__ void kern(double *out, long long *cyc, int iters) {
     float fa = 1.0f + threadIdx.x * 1e-6f, fb = 0.9999f, fc = 1e-7f;
     int ia = threadIdx.x, ib = 3;
     unsigned addr = (threadIdx.x & 63) * 8;
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    f2v pa = {fa, fa}, pb = {0.9999f, 1.0001f}, pc = pa, pd = pa, pe = pa;
     long long t0 = __builtin_amdgcn_s_memtime();
     for (int it = 0; it < iters; ++it) {
         if (V == 0) {   // dependent v_fma_f64 chain
@@ -49,6 +51,22 @@ __global__ void kern(double *out, long long *cyc, int iters) {
             REP64(asm volatile("v_cvt_f64_f32 %0, %1\n\tv_cvt_f32_f64 %1, %0" : "+v"(a), "+v"(fa));)
         } else if (V == 11) {  // dependent v_add_f64 chain
             REP64(asm volatile("v_add_f64 %0, %0, %1" : "+v"(a) : "v"(b));)
+        } else if (V == 13) {  // dependent v_pk_add_f32 chain
+            REP64(asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(pa) : "v"(pb));)
+        } else if (V == 14) {  // dependent v_pk_mul_f32 chain
+            REP64(asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(pa) : "v"(pb));)
+        } else if (V == 15) {  // dependent v_add_f32 chain
+            REP64(asm volatile("v_add_f32 %0, %0, %1" : "+v"(fa) : "v"(fb));)
+        } else if (V == 16) {  // dependent v_add_f32_dpp row_shr:2 chain (2 wait states each)
+            REP64(asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %1 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(fa) : "v"(fb));)
+        } else if (V == 17) {  // 4 independent v_pk_add_f32 chains, interleaved
+            REP8(REP8(asm volatile("v_pk_add_f32 %0, %0, %4\n\tv_pk_add_f32 %1, %1, %4\n\t"
+                                   "v_pk_add_f32 %2, %2, %4\n\tv_pk_add_f32 %3, %3, %4"
+                                   : "+v"(pa), "+v"(pc), "+v"(pd), "+v"(pe) : "v"(pb));))
+        } else if (V == 18) {  // dependent pk_add with op_sel swap + neg (the FLL combine)
+            REP64(asm volatile("v_pk_add_f32 %0, %0, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "+v"(pa) : "v"(pb));)
+        } else if (V == 19) {  // dependent v_cvt_f32_f64 -> v_pk_mul_f32 (f64 result into packed)
+            REP64(asm volatile("v_cvt_f64_f32 %0, %1\n\tv_pk_mul_f32 %2, %2, %3\n\tv_cvt_f32_f64 %1, %0" : "+v"(a), "+v"(fa), "+v"(pa) : "v"(pb));)
         } else if (V == 12) {  // scalar op stream (s_mov: leaves SCC, which the loop branch uses, alone)
             int sa = it, sb = 7;
             REP64(asm volatile("s_mov_b32 %0, %1" : "=s"(sa) : "s"(sb));)
@@ -56,7 +74,7 @@ __global__ void kern(double *out, long long *cyc, int iters) {
         }
     }
     long long t1 = __builtin_amdgcn_s_memtime();
-    out[threadIdx.x + blockIdx.x * blockDim.x] = a + d + e + f + fa + ia + addr;
+    out[threadIdx.x + blockIdx.x * blockDim.x] = a + d + e + f + fa + ia + addr + pa.x + pc.y + pd.x + pe.y;
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
@@ -67,7 +85,9 @@ int main() {
     const char *names[] = {"dep fma_f64", "4x indep fma_f64", "dep fma_f32", "4x indep fma_f32",
                            "dep add_u32", "dep ds_read_b32+wait", "2 chains fma_f64",
                            "dep mul_f64", "fma_f64 + cndmask", "dep floor_f64",
-                           "cvt f32<->f64 pair", "dep add_f64", "scalar s_add"};
+                           "cvt f32<->f64 pair", "dep add_f64", "scalar s_add", "dep pk_add_f32",
+                           "dep pk_mul_f32", "dep add_f32", "dep add_f32_dpp+nop1", "4x indep pk_add",
+                           "dep pk_add opsel/neg", "cvt>pk_mul>cvt"};
     const int iters = 1000;
     auto run = [&](auto kfn, int idx, int waves_per_block, int blocks) {
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * waves_per_block), 0, 0, out, cyc, 10);
@@ -82,7 +102,9 @@ int main() {
         run(kern<0>, 0, w, 1); run(kern<1>, 1, w, 1); run(kern<2>, 2, w, 1); run(kern<3>, 3, w, 1);
         run(kern<4>, 4, w, 1); run(kern<5>, 5, w, 1); run(kern<6>, 6, w, 1); run(kern<7>, 7, w, 1);
         run(kern<8>, 8, w, 1); run(kern<9>, 9, w, 1); run(kern<10>, 10, w, 1); run(kern<11>, 11, w, 1);
-        run(kern<12>, 12, w, 1);
+        run(kern<12>, 12, w, 1); run(kern<13>, 13, w, 1); run(kern<14>, 14, w, 1);
+        run(kern<15>, 15, w, 1); run(kern<16>, 16, w, 1); run(kern<17>, 17, w, 1);
+        run(kern<18>, 18, w, 1); run(kern<19>, 19, w, 1);
     }
     // s_memtime rate: ticks over a wall-clock interval
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
