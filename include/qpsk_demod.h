@@ -102,6 +102,33 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
                        int64_t bits_stride_bytes, int64_t *n_bits, float *syms,
                        int64_t syms_stride_floats, int64_t *n_syms);
 
+/*
+ * Pipelined DeModulate calls (device memory only).  Same arguments, checks and
+ * results as qpsk_demod_process(mem = QPSK_MEM_DEVICE); calls still apply to
+ * every stream in order and carry the state exactly as synchronous calls do.
+ * The difference is scheduling: each call is split into a front stage (FLL on:
+ * the FLL; FLL off: the matched filter) and a back stage (the rest) on two
+ * library streams, so call k+1's front stage runs while call k's symbol loop
+ * runs.  A C# host feeding consecutive SDR buffers keeps the GPU busy this
+ * way instead of waiting for each DeModulate to return.
+ *  - iq is read after the work already queued on the handle's stream; it must
+ *    stay unchanged until qpsk_demod_pipeline_wait has been called for it.
+ *  - bits / n_bits / syms / n_syms are complete after qpsk_demod_pipeline_wait.
+ *  - synchronous process(), get/set_state, set_stream and destroy first wait
+ *    for every pipelined call.
+ */
+int qpsk_demod_process_async(qpsk_demod *h, int32_t mode, const float *iq, int64_t stride_floats,
+                             int64_t n_samples, const int64_t *lengths, uint8_t *bits,
+                             int64_t bits_stride_bytes, int64_t *n_bits, float *syms,
+                             int64_t syms_stride_floats, int64_t *n_syms);
+/* Make hip_stream wait for every pipelined call issued so far (NULL: block the
+ * calling host thread until they are done). */
+int qpsk_demod_pipeline_wait(qpsk_demod *h, void *hip_stream);
+/* 2 = the stage boundary is double-buffered (front and back stages overlap),
+ * 1 = no device memory was left for the second buffer (stages serialise),
+ * 0 = no pipelined call yet. */
+int qpsk_demod_pipeline_depth(const qpsk_demod *h);
+
 /* Upper bounds a caller sizes outputs with, for a call of n_samples per stream. */
 int64_t qpsk_demod_max_symbols(const qpsk_demod *h, int64_t n_samples);
 

@@ -262,14 +262,14 @@ __global__ __launch_bounds__(64) void fll_kernel(FllArgs a, FllParams P) {
     const int64_t n = a.lengths ? a.lengths[s] : a.n;
     if (n == 0) return;
     constexpr int N = kFllTaps;
-    StreamState st = a.state[s];
+    const StreamState *st_in = a.state + s;
     const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
     f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride;
     // 2N delay line (FIRFilter.cs:18-22), shared by both band-edge filters since
     // both are fed the same mixed sample.
     f2 *dl = reinterpret_cast<f2 *>(a.delay) + static_cast<int64_t>(s) * 2 * N;
-    float phase = st.fll_phase, freq = st.fll_freq;
-    int pos = st.fll_pos;
+    float phase = st_in->fll_phase, freq = st_in->fll_freq;
+    int pos = st_in->fll_pos;
     const float two_pi = 2.0f * 3.14159274101257324219f;
     for (int64_t t = 0; t < n; ++t) {
         const f2 in = x[t];
@@ -296,10 +296,11 @@ __global__ __launch_bounds__(64) void fll_kernel(FllArgs a, FllParams P) {
         ++pos;
         if (pos == N) pos = 0;
     }
-    st.fll_phase = phase;
-    st.fll_freq = freq;
-    st.fll_pos = pos;
-    a.state[s] = st;
+    // only the FLL's own fields: in pipelined calls the loop kernel of the
+    // previous call may be writing the M&M/Costas fields of this struct
+    a.state[s].fll_phase = phase;
+    a.state[s].fll_freq = freq;
+    a.state[s].fll_pos = pos;
 }
 
 // ---------------------------------------------------------------------------

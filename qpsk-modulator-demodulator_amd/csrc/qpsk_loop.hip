@@ -70,6 +70,30 @@ constexpr int kCapSps2 = 40;
 constexpr int kCap128Sps2 = 72;
 typedef double d2 __attribute__((ext_vector_type(2)));
 
+// M&M -> Costas symbol slots: doubles (default; the M&M wave has them widened
+// already) or floats (QPSK_SYM_F32=1: 21 KB less LDS, widened by the Costas
+// wave).  Same results; A/B on one MI355X (C3, serial calls): doubles 45.6 ms,
+// floats 47.6 ms per loop launch, so the smaller footprint -- which would let
+// one matched-filter workgroup of the next pipelined call share the CU -- does
+// not pay for the two extra conversions on the Costas wave
+#ifndef QPSK_SYM_F32
+#define QPSK_SYM_F32 0
+#endif
+#if QPSK_SYM_F32
+typedef f2 sym_t;
+__device__ __forceinline__ sym_t to_sym(float ci, float cq, double, double) { return f2{ci, cq}; }
+__device__ __forceinline__ d2 from_sym(f2 v) { return d2{static_cast<double>(v.x), static_cast<double>(v.y)}; }
+__device__ __forceinline__ f2 sym_to_f2(f2 v) { return v; }
+#else
+typedef d2 sym_t;
+__device__ __forceinline__ sym_t to_sym(float, float, double cid, double cqd) { return d2{cid, cqd}; }
+__device__ __forceinline__ d2 from_sym(d2 v) { return v; }
+__device__ __forceinline__ f2 sym_to_f2(d2 v) { return f2{static_cast<float>(v.x), static_cast<float>(v.y)}; }
+#endif
+#ifndef QPSK_LOOP_PRIO
+#define QPSK_LOOP_PRIO 3
+#endif
+
 __device__ __forceinline__ int wave_max_i32(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -107,7 +131,7 @@ struct LoopLds {
     double tab[1024];              // sincos table head (qpsk_sincos.h), at LDS offset 0 so
     double tab_lo[1024];           // the table index is the whole address; tail (floats, widened)
     f2 mf[SPW * Ring<KB>::row];    // sample ring   [stream][mirror | 4 rounds x KB]
-    d2 sym[2 * SPW * RS];          // M&M -> Costas [slot][stream][RS], widened to double
+    sym_t sym[2 * SPW * RS];       // M&M -> Costas [slot][stream][RS] (see sym_t)
     f2 rot[2 * SPW * RS];          // Costas -> decode
     int cnt[4 * SPW + 4];          // symbols produced by the M&M in round r: cnt[r & 3];
                                    // cnt[4*SPW + (r & 3)] = their minimum over the batch
@@ -124,6 +148,10 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     const int lane = threadIdx.x & 63;
     const int s = blockIdx.x * SPW + lane;
     const bool valid = lane < SPW && s < a.S;
+    // every wave here runs a latency-bound chain: should a pipelined call's
+    // front-stage workgroups share a SIMD with them, these waves win VALU
+    // arbitration
+    __builtin_amdgcn_s_setprio(QPSK_LOOP_PRIO);
 
     // ---- per-stream queue geometry (every wave: lane l <-> stream blk*SPW + l)
     int n = 0, cnt = 0, R = 0, d = 0;
@@ -239,9 +267,9 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         for (int r = 0; r <= NR + 1; ++r) {
             __builtin_amdgcn_s_barrier();
             if (r >= NR) continue;
-            d2 *out = L.sym + ((r & 1) * SPW + lane) * L.RS;
+            sym_t *out = L.sym + ((r & 1) * SPW + lane) * L.RS;
             if (lane < SPW)
-                for (int k = 0; k < 8; ++k) out[k] = d2{0.7 + 0.01 * k, -0.7 + 0.02 * k};
+                for (int k = 0; k < 8; ++k) out[k] = to_sym(0.7f, -0.7f, 0.7 + 0.01 * k, -0.7 + 0.02 * k);
             if (lane < SPW) L.cnt[(r & 3) * SPW + lane] = mine ? 8 : 0;
             if (lane == 0) L.cnt[4 * SPW + (r & 3)] = 8;
         }
@@ -309,7 +337,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 row[2] = row[kMir + kRing - 2]; row[3] = row[kMir + kRing - 1];
             }
             const int rend = (r + 1) * KB < cnt ? (r + 1) * KB : cnt;
-            d2 *out = L.sym + ((r & 1) * SPW + lane) * L.RS;
+            sym_t *out = L.sym + ((r & 1) * SPW + lane) * L.RS;
             int kmax = stop ? 0 : (cap - nsym < CAP ? cap - nsym : CAP);
             int k = 0, kuni = 0;
             lds_f2 *tp = (lds_f2 *)taps(base);
@@ -357,7 +385,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 interp(ci, cq);
                 has_prev = 1;
                 psid = ci; psqd = cq;
-                out[k++] = d2{psid, psqd};
+                out[k++] = to_sym(ci, cq, psid, psqd);
                 psi = ci; psq = cq;
                 pdid = ci >= 0.0f ? 1.0 : -1.0;
                 pdqd = cq >= 0.0f ? 1.0 : -1.0;
@@ -380,7 +408,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 // which the reference cannot survive either, clamps instead of
                 // propagating)
                 const double corr = __builtin_fmax(__builtin_fmin(c, 0.1), -0.1);
-                out[k++] = d2{cid, cqd};
+                out[k++] = to_sym(ci, cq, cid, cqd);
                 psid = cid; psqd = cqd;
                 pdid = did; pdqd = dqd;
                 advance(sps + corr, load);
@@ -528,8 +556,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             const int slot = (r - 1) & 1;
             const int m = mine ? L.cnt[((r - 1) & 3) * SPW + lane] : 0;
             for (int k = 0; k < m; ++k) {
-                const d2 y = L.sym[(slot * SPW + lane) * L.RS + k];
-                L.rot[(slot * SPW + lane) * L.RS + k] = f2{static_cast<float>(y.x), static_cast<float>(y.y)};
+                L.rot[(slot * SPW + lane) * L.RS + k] = sym_to_f2(L.sym[(slot * SPW + lane) * L.RS + k]);
             }
         }
         return;
@@ -565,14 +592,15 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             const int mlo = __builtin_amdgcn_readfirstlane(L.cnt[4 * SPW + ((r - 1) & 3)]);
             if (lane >= SPW) continue;   // exec = the batch's lanes for the whole round
             const int m = mine ? L.cnt[((r - 1) & 3) * SPW + lane] : 0;
-            const d2 *in = L.sym + (slot * SPW + lane) * L.RS;
+            const sym_t *in = L.sym + (slot * SPW + lane) * L.RS;
             f2 *out = L.rot + (slot * SPW + lane) * L.RS;
             d2 y;
-            // CostasLoopQpsk.cs:63-92: double NCO, float I/O (y already widened).
+            // CostasLoopQpsk.cs:63-92: double NCO, float I/O (y widened to double).
             // HUGE: theta may exceed the table reduction's range (qpsk_sincos_arg);
             // the fast pass assumes it does not and the round is redone if it did.
+            auto widen = [](sym_t v) { return from_sym(v); };
             auto step = [&](int k, auto huge) {
-                const d2 yn = in[k + 1];   // next symbol, read under this one's chain
+                const d2 yn = widen(in[k + 1]);   // next symbol, read and widened under this one's chain
                 double sn, cs;
                 if constexpr (decltype(huge)::value) qpsk_sincos_tab(theta, L.tab, L.tab_lo, &sn, &cs);
                 else qpsk_sincos_tab_core_k(theta, L.tab, L.tab_lo, &K, &sn, &cs);
@@ -594,7 +622,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 y = yn;
             };
             const double theta0 = theta, freq0 = freq;
-            y = in[0];
+            y = widen(in[0]);
             int k = 0;
             double amax = fabs(theta);   // largest sincos argument of the round
             STAMP(tu);
@@ -618,7 +646,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             if (__builtin_expect(__ballot(mine && amax > 1.0e6) != 0, 0)) {
                 theta = theta0;
                 freq = freq0;
-                y = in[0];
+                y = widen(in[0]);
                 for (k = 0; k < m; ++k) step(k, std::true_type{});
             }
             ACC(k_loop, tl);

@@ -1,17 +1,30 @@
 // qpsk_runtime.hip -- host runtime behind the C ABI (include/qpsk_demod.h):
 // handle = a batch of S reference QPSKDeModulator instances living on one
 // MI355X.  Owns the device buffers and the per-stream state, orders the kernels
-// of one DeModulate call on one HIP stream:
+// of one DeModulate call:
 //
 //     [FLL] -> matched-filter FIR -> FIR history carry -> M&M+Costas+decode
+//
+// qpsk_demod_process runs them on the handle's stream.  qpsk_demod_process_async
+// splits each call into a front and a back stage on two library streams so
+// that call k+1's front stage overlaps call k's back stage:
+//
+//     FLL off:  front = FIR + history        back = carry + loop kernel + copies
+//     FLL on:   front = FLL                  back = FIR + history + carry + loop
+//
+// What the two stages share: the per-stream StreamState (its FLL fields are
+// written only by the FLL, every other field only by the loop kernel), and the
+// buffer at the stage boundary (MF rows, or FLL output rows), which is
+// double-buffered (fll_out[2] / mf[2]; the second only when pipelined).
 //
 // Device layout (HBM, stream-major so every stage reads/writes each stream's
 // time axis contiguously):
 //   in      [S][n_max]              float2  staging for host input
-//   fll_out [S][n_max]              float2  (FLL mode)
+//   fll_out [2][S][n_max]           float2  (FLL mode; the 2nd only when pipelined)
 //   hist    2 x [S][T-1]            float2  FIR delay line (ping-pong)
-//   mf      [S][64 + n_max]         float2  matched-filter output; the 64-slot
-//                                           prefix receives the M&M carry
+//   mf      [2][S][64 + n_max]      float2  matched-filter output; the 64-slot
+//                                           prefix receives the M&M carry (the
+//                                           2nd only when pipelined, FLL off)
 //   carry   [S][64]                 float2  M&M retained samples
 //   state   [S]                     StreamState
 //   bits    [S][words]              uint32  MSB-first packed bits
@@ -56,6 +69,8 @@ int dev_alloc(T **p, size_t count) {
         return fail(QPSK_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
     return QPSK_OK;
 }
+
+constexpr int kEv = 6;
 }  // namespace
 
 namespace qpsk {
@@ -81,24 +96,243 @@ struct qpsk_demod {
     int64_t syms_cap = 0;        // per stream
     float *d_hrev = nullptr;
     float *d_in = nullptr;
-    float *d_fll_out = nullptr;
+    float *d_fll_out[2] = {nullptr, nullptr};
     float *d_hist[2] = {nullptr, nullptr};
     int hist_cur = 0;
-    float *d_mf = nullptr;
+    float *d_mf[2] = {nullptr, nullptr};
     float *d_carry = nullptr;
     StreamState *d_state = nullptr;
     float *d_fll_delay = nullptr;
     uint32_t *d_bits = nullptr;
     float *d_syms = nullptr;
     int64_t *d_counts = nullptr;     // [2][S]: n_bits, n_syms
-    int64_t *d_lengths = nullptr;
+    int64_t *d_lengths[2] = {nullptr, nullptr};
     int64_t *h_counts = nullptr;     // pinned
     bool timing = false;
-    // one set of 5 events per timed call: start, after FLL, after FIR, after
-    // FIR-history, after loop kernel; averaged by qpsk_demod_stage_times()
-    std::vector<std::array<hipEvent_t, 5>> ev_pool;
+    // one set of kEv events per timed call (start, FLL end, FIR start, FIR end,
+    // loop start, loop end), each on the stream its stage runs on; averaged by
+    // qpsk_demod_stage_times()
+    std::vector<std::array<hipEvent_t, kEv>> ev_pool;
     size_t ev_used = 0;
+    // ---- pipelined calls (qpsk_demod_process_async) ----------------------
+    bool pipe_ready = false;
+    int pipe_bufs = 0;               // 2 = double-buffered stage boundary, 1 = no room for it
+    int pipe_cur = 0;
+    hipStream_t s_front = nullptr, s_back = nullptr;
+    hipEvent_t e_in = nullptr;
+    hipEvent_t e_front[2] = {nullptr, nullptr}, e_back[2] = {nullptr, nullptr};
+    bool front_rec[2] = {false, false}, back_rec[2] = {false, false};
+    int last_back = -1;              // boundary buffer of the newest back stage, -1 = none
+    int64_t *h_len[2] = {nullptr, nullptr};   // pinned staging of per-call lengths
 };
+
+namespace {
+
+// The newest pipelined call's back stage, or nullptr.
+hipEvent_t last_async(const qpsk_demod *h) { return h->last_back >= 0 ? h->e_back[h->last_back] : nullptr; }
+
+// Host wait for every pipelined call issued so far.
+int drain_async(const qpsk_demod *h) {
+    if (hipEvent_t e = last_async(h)) HIP_TRY(hipEventSynchronize(e));
+    return QPSK_OK;
+}
+
+struct Call {
+    int32_t mode;
+    const float *iq;
+    int64_t stride_floats;
+    int64_t n_samples;
+    const int64_t *lengths;
+    int32_t mem;
+    uint8_t *bits;
+    int64_t bits_stride_bytes;
+    int64_t *n_bits;
+    float *syms;
+    int64_t syms_stride_floats;
+    int64_t *n_syms;
+    int64_t n_call = 0;    // derived by validate()
+    int64_t max_sym = 0;
+};
+
+int validate(qpsk_demod *h, Call &c) {
+    if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
+    if (c.mode != QPSK_MODE_DEMODULATE && c.mode != QPSK_MODE_CONSTELLATION)
+        return fail(QPSK_ERR_ARGUMENT, "unknown mode");
+    if (c.mem != QPSK_MEM_HOST && c.mem != QPSK_MEM_DEVICE) return fail(QPSK_ERR_ARGUMENT, "unknown mem");
+    const int S = h->S;
+    int64_t n_call = 0;
+    if (c.lengths) {
+        for (int s = 0; s < S; ++s) {
+            if (c.lengths[s] < 0) return fail(QPSK_ERR_ARGUMENT, "negative length");
+            n_call = std::max(n_call, c.lengths[s]);
+        }
+    } else {
+        if (c.n_samples < 0) return fail(QPSK_ERR_ARGUMENT, "negative n_samples");
+        n_call = c.n_samples;
+    }
+    if (n_call > h->n_max) return fail(QPSK_ERR_CAPACITY, "call longer than max_samples_per_call");
+    if (n_call > 0 && !c.iq) return fail(QPSK_ERR_ARGUMENT_NULL, "SamplesIQ is null");
+    if (n_call > 0 && c.stride_floats < 2 * n_call) return fail(QPSK_ERR_ARGUMENT, "stride too small");
+    if (c.mode == QPSK_MODE_DEMODULATE && (!c.bits || !c.n_bits))
+        return fail(QPSK_ERR_ARGUMENT_NULL, "bits / n_bits required");
+    if (c.mode == QPSK_MODE_CONSTELLATION && (!c.syms || !c.n_syms))
+        return fail(QPSK_ERR_ARGUMENT_NULL, "syms / n_syms required");
+    const int64_t max_sym = qpsk_demod_max_symbols(h, n_call);
+    if (c.bits && c.bits_stride_bytes < ((2 * max_sym + 7) / 8))
+        return fail(QPSK_ERR_ARGUMENT, "bits_stride_bytes smaller than 2*max_symbols/8");
+    if (c.syms && c.syms_stride_floats < 2 * max_sym)
+        return fail(QPSK_ERR_ARGUMENT, "syms_stride_floats smaller than 2*max_symbols");
+    if (n_call > 0 && c.mem == QPSK_MEM_DEVICE && (c.stride_floats & 1))
+        return fail(QPSK_ERR_ARGUMENT, "device stride_floats must be even");
+    int rc;
+    if (c.syms && !h->d_syms) {
+        if ((rc = dev_alloc(&h->d_syms, static_cast<size_t>(2 * S * h->syms_cap)))) return rc;
+    }
+    c.n_call = n_call;
+    c.max_sym = max_sym;
+    return QPSK_OK;
+}
+
+hipEvent_t *next_events(qpsk_demod *h, int *rc) {
+    *rc = QPSK_OK;
+    if (!h->timing) return nullptr;
+    if (h->ev_used == h->ev_pool.size()) {
+        std::array<hipEvent_t, kEv> set{};
+        for (auto &e : set) {
+            if (hipEventCreate(&e) != hipSuccess) {
+                *rc = fail(QPSK_ERR_DEVICE, "hipEventCreate");
+                return nullptr;
+            }
+        }
+        h->ev_pool.push_back(set);
+    }
+    return h->ev_pool[h->ev_used++].data();
+}
+
+}  // namespace (validation)
+
+namespace {
+
+#define EV(i, st)                                      \
+    do {                                               \
+        if (ev) HIP_TRY(hipEventRecord(ev[i], (st)));  \
+    } while (0)
+
+// FLL (Band-Edge Filter.cs:64-87), README order FLL -> MF
+void run_fll(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_len, int64_t n_call,
+             float *y, hipStream_t st) {
+    FllArgs fa{};
+    fa.x = x; fa.x_stride = x_stride;
+    fa.y = y; fa.y_stride = h->n_max;
+    fa.delay = h->d_fll_delay;
+    fa.lengths = d_len; fa.n = n_call;
+    fa.state = h->d_state; fa.S = h->S;
+    launch_fll(fa, h->fp, st);
+}
+
+// matched filter (QPSKDeModulator.cs:360) + FIR delay-line carry
+int run_fir(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_len, int64_t n_call,
+            float *mf, hipStream_t st, hipEvent_t *ev) {
+    FirArgs fa{};
+    fa.x = x; fa.x_stride = x_stride;
+    fa.hist = h->d_hist[h->hist_cur];
+    fa.lengths = d_len; fa.n = n_call;
+    fa.y = mf; fa.y_stride = h->mf_stride; fa.y_offset = kMfPrefix;
+    EV(2, st);
+    if (n_call > 0) {
+        launch_fir(fa, h->taps, h->d_hrev, h->T, h->W, h->S, n_call, st);
+        EV(3, st);
+        launch_fir_hist(fa, h->d_hist[h->hist_cur ^ 1], h->T - 1, h->S, st);
+        h->hist_cur ^= 1;
+    } else {
+        EV(3, st);
+    }
+    return QPSK_OK;
+}
+
+// symbol sync + Costas + decode (QPSKDeModulator.cs:364-408) and the output copies
+int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipStream_t st,
+             hipEvent_t *ev) {
+    const int S = h->S;
+    EV(4, st);
+    LoopArgs la{};
+    la.mf = mf; la.mf_stride = h->mf_stride;
+    la.carry = h->d_carry;
+    la.lengths = d_len; la.n = c.n_call;
+    la.state = h->d_state;
+    la.bits = c.mode == QPSK_MODE_DEMODULATE ? h->d_bits : nullptr;
+    la.bits_stride_words = h->bits_words;
+    la.bits_cap_words = h->bits_words;
+    la.n_bits = h->d_counts;
+    la.syms = c.syms ? h->d_syms : nullptr;
+    la.syms_stride = h->syms_cap;
+    la.syms_cap = h->syms_cap;
+    la.n_syms = h->d_counts + S;
+    la.S = S;
+    launch_loop(la, h->lp, c.mode, h->loop_variant, st);
+    HIP_TRY(hipGetLastError());
+    EV(5, st);
+    const hipMemcpyKind kind = c.mem == QPSK_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    const int64_t bytes_row = (2 * c.max_sym + 7) / 8;
+    if (c.bits && bytes_row > 0)
+        HIP_TRY(hipMemcpy2DAsync(c.bits, c.bits_stride_bytes, h->d_bits, h->bits_words * 4, bytes_row, S, kind, st));
+    if (c.syms && c.max_sym > 0)
+        HIP_TRY(hipMemcpy2DAsync(c.syms, c.syms_stride_floats * sizeof(float), h->d_syms,
+                                 2 * h->syms_cap * sizeof(float), 2 * c.max_sym * sizeof(float), S, kind, st));
+    if (c.mem == QPSK_MEM_HOST) {
+        HIP_TRY(hipMemcpyAsync(h->h_counts, h->d_counts, 2 * S * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (c.n_bits) std::memcpy(c.n_bits, h->h_counts, S * sizeof(int64_t));
+        if (c.n_syms) std::memcpy(c.n_syms, h->h_counts + S, S * sizeof(int64_t));
+    } else {
+        if (c.n_bits) HIP_TRY(hipMemcpyAsync(c.n_bits, h->d_counts, S * sizeof(int64_t), kind, st));
+        if (c.n_syms) HIP_TRY(hipMemcpyAsync(c.n_syms, h->d_counts + S, S * sizeof(int64_t), kind, st));
+    }
+    return QPSK_OK;
+}
+
+}  // namespace (stage runners)
+
+namespace {
+
+// Streams, events and the second stage-boundary buffer of the pipelined path.
+// The back stream gets the device's highest priority: its loop kernel is the
+// latency-bound stage, the front stage fills the CUs it leaves idle.
+int pipe_setup(qpsk_demod *h) {
+    if (h->pipe_ready) return QPSK_OK;
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_TRY(hipStreamCreateWithPriority(&h->s_front, hipStreamNonBlocking, least));
+    HIP_TRY(hipStreamCreateWithPriority(&h->s_back, hipStreamNonBlocking, greatest));
+    HIP_TRY(hipEventCreateWithFlags(&h->e_in, hipEventDisableTiming));
+    for (int b = 0; b < 2; ++b) {
+        HIP_TRY(hipEventCreateWithFlags(&h->e_front[b], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&h->e_back[b], hipEventDisableTiming));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h->h_len[b]), h->S * sizeof(int64_t)));
+    }
+    int rc;
+    if (!h->d_lengths[1] && (rc = dev_alloc(&h->d_lengths[1], h->S))) return rc;
+    // the second boundary buffer: FLL output rows with the FLL on, MF rows
+    // otherwise.  No room for it (batches near the 288 GB) -> calls still
+    // queue back to back, but each front stage waits for the previous back stage
+    const size_t S = static_cast<size_t>(h->S);
+    hipError_t e;
+    if (h->p.enable_fll)
+        e = hipMalloc(reinterpret_cast<void **>(&h->d_fll_out[1]), 2 * S * h->n_max * sizeof(float));
+    else
+        e = hipMalloc(reinterpret_cast<void **>(&h->d_mf[1]), 2 * S * h->mf_stride * sizeof(float));
+    if (e == hipSuccess) {
+        h->pipe_bufs = 2;
+        if (!h->p.enable_fll) HIP_TRY(hipMemset(h->d_mf[1], 0, 2 * S * h->mf_stride * sizeof(float)));
+    } else {
+        (void)hipGetLastError();
+        h->pipe_bufs = 1;
+    }
+    h->pipe_ready = true;
+    return QPSK_OK;
+}
+
+}  // namespace (pipeline setup)
 
 extern "C" {
 
@@ -208,13 +442,13 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
     const int H = h->T - 1;
     if ((rc = dev_alloc(&h->d_hrev, h->T)) || (rc = dev_alloc(&h->d_hist[0], 2 * S * H)) ||
         (rc = dev_alloc(&h->d_hist[1], 2 * S * H)) ||
-        (rc = dev_alloc(&h->d_mf, static_cast<size_t>(2 * S * h->mf_stride))) ||
+        (rc = dev_alloc(&h->d_mf[0], static_cast<size_t>(2 * S * h->mf_stride))) ||
         (rc = dev_alloc(&h->d_carry, 2 * S * kCarryMax)) || (rc = dev_alloc(&h->d_state, S)) ||
         (rc = dev_alloc(&h->d_fll_delay, 2 * S * 2 * kFllTaps)) ||
         (rc = dev_alloc(&h->d_bits, static_cast<size_t>(S * h->bits_words))) ||
-        (rc = dev_alloc(&h->d_counts, 2 * S)) || (rc = dev_alloc(&h->d_lengths, S)))
+        (rc = dev_alloc(&h->d_counts, 2 * S)) || (rc = dev_alloc(&h->d_lengths[0], S)))
         return cleanup_fail(rc);
-    if (p->enable_fll && (rc = dev_alloc(&h->d_fll_out, static_cast<size_t>(2 * S * h->n_max))))
+    if (p->enable_fll && (rc = dev_alloc(&h->d_fll_out[0], static_cast<size_t>(2 * S * h->n_max))))
         return cleanup_fail(rc);
     if (hipHostMalloc(reinterpret_cast<void **>(&h->h_counts), 2 * S * sizeof(int64_t)) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipHostMalloc"));
@@ -232,7 +466,7 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
         (H > 0 && hipMemset(h->d_hist[0], 0, 2 * S * H * sizeof(float)) != hipSuccess) ||
         hipMemset(h->d_carry, 0, 2 * S * kCarryMax * sizeof(float)) != hipSuccess ||
         hipMemset(h->d_fll_delay, 0, 2 * S * 2 * kFllTaps * sizeof(float)) != hipSuccess ||
-        hipMemset(h->d_mf, 0, static_cast<size_t>(2 * S * h->mf_stride) * sizeof(float)) != hipSuccess)
+        hipMemset(h->d_mf[0], 0, static_cast<size_t>(2 * S * h->mf_stride) * sizeof(float)) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "device init failed"));
     *out = h;
     return QPSK_OK;
@@ -240,23 +474,31 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
 
 int qpsk_demod_destroy(qpsk_demod *h) {
     if (!h) return QPSK_OK;
+    drain_async(h);
     if (h->stream) hipStreamSynchronize(h->stream);
     hipFree(h->d_hrev);
     hipFree(h->d_in);
-    hipFree(h->d_fll_out);
-    hipFree(h->d_hist[0]);
-    hipFree(h->d_hist[1]);
-    hipFree(h->d_mf);
+    for (int b = 0; b < 2; ++b) {
+        hipFree(h->d_fll_out[b]);
+        hipFree(h->d_hist[b]);
+        hipFree(h->d_mf[b]);
+        hipFree(h->d_lengths[b]);
+        if (h->h_len[b]) hipHostFree(h->h_len[b]);
+        if (h->e_front[b]) hipEventDestroy(h->e_front[b]);
+        if (h->e_back[b]) hipEventDestroy(h->e_back[b]);
+    }
     hipFree(h->d_carry);
     hipFree(h->d_state);
     hipFree(h->d_fll_delay);
     hipFree(h->d_bits);
     hipFree(h->d_syms);
     hipFree(h->d_counts);
-    hipFree(h->d_lengths);
     if (h->h_counts) hipHostFree(h->h_counts);
     for (auto &set : h->ev_pool)
         for (auto &e : set) hipEventDestroy(e);
+    if (h->e_in) hipEventDestroy(h->e_in);
+    if (h->s_front) hipStreamDestroy(h->s_front);
+    if (h->s_back) hipStreamDestroy(h->s_back);
     if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
     delete h;
     return QPSK_OK;
@@ -264,6 +506,8 @@ int qpsk_demod_destroy(qpsk_demod *h) {
 
 int qpsk_demod_set_stream(qpsk_demod *h, void *hip_stream) {
     if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
+    int rc;
+    if ((rc = drain_async(h))) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
     if (hip_stream) {
         if (h->own_stream) hipStreamDestroy(h->stream);
@@ -286,14 +530,14 @@ int qpsk_demod_enable_timing(qpsk_demod *h, int32_t on) {
 int qpsk_demod_stage_times(const qpsk_demod *h, float *ms, int32_t n) {
     if (!h || !ms) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
     float sum[4] = {0, 0, 0, 0};
-    if (h->ev_used > 0) HIP_TRY(hipEventSynchronize(h->ev_pool[h->ev_used - 1][4]));
+    for (size_t c = 0; c < h->ev_used; ++c) HIP_TRY(hipEventSynchronize(h->ev_pool[c][kEv - 1]));
     for (size_t c = 0; c < h->ev_used; ++c) {
         const auto &e = h->ev_pool[c];
         float t;
         HIP_TRY(hipEventElapsedTime(&t, e[0], e[1])); sum[0] += t;
-        HIP_TRY(hipEventElapsedTime(&t, e[1], e[2])); sum[1] += t;
-        HIP_TRY(hipEventElapsedTime(&t, e[3], e[4])); sum[2] += t;
-        HIP_TRY(hipEventElapsedTime(&t, e[0], e[4])); sum[3] += t;
+        HIP_TRY(hipEventElapsedTime(&t, e[2], e[3])); sum[1] += t;
+        HIP_TRY(hipEventElapsedTime(&t, e[4], e[5])); sum[2] += t;
+        HIP_TRY(hipEventElapsedTime(&t, e[0], e[5])); sum[3] += t;
     }
     const int k = std::min<int32_t>(n, 4);
     for (int i = 0; i < k; ++i) ms[i] = h->ev_used ? sum[i] / h->ev_used : 0.f;
@@ -304,49 +548,19 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
                        int64_t n_samples, const int64_t *lengths, int32_t mem, uint8_t *bits,
                        int64_t bits_stride_bytes, int64_t *n_bits, float *syms,
                        int64_t syms_stride_floats, int64_t *n_syms) {
-    if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
-    if (mode != QPSK_MODE_DEMODULATE && mode != QPSK_MODE_CONSTELLATION)
-        return fail(QPSK_ERR_ARGUMENT, "unknown mode");
-    if (mem != QPSK_MEM_HOST && mem != QPSK_MEM_DEVICE) return fail(QPSK_ERR_ARGUMENT, "unknown mem");
-    const int S = h->S;
-    int64_t n_call = 0;
-    if (lengths) {
-        for (int s = 0; s < S; ++s) {
-            if (lengths[s] < 0) return fail(QPSK_ERR_ARGUMENT, "negative length");
-            n_call = std::max(n_call, lengths[s]);
-        }
-    } else {
-        if (n_samples < 0) return fail(QPSK_ERR_ARGUMENT, "negative n_samples");
-        n_call = n_samples;
-    }
-    if (n_call > h->n_max) return fail(QPSK_ERR_CAPACITY, "call longer than max_samples_per_call");
-    if (n_call > 0 && !iq) return fail(QPSK_ERR_ARGUMENT_NULL, "SamplesIQ is null");
-    if (n_call > 0 && stride_floats < 2 * n_call) return fail(QPSK_ERR_ARGUMENT, "stride too small");
-    if (mode == QPSK_MODE_DEMODULATE && (!bits || !n_bits))
-        return fail(QPSK_ERR_ARGUMENT_NULL, "bits / n_bits required");
-    if (mode == QPSK_MODE_CONSTELLATION && (!syms || !n_syms))
-        return fail(QPSK_ERR_ARGUMENT_NULL, "syms / n_syms required");
-    const int64_t max_sym = qpsk_demod_max_symbols(h, n_call);
-    if (bits && bits_stride_bytes < ((2 * max_sym + 7) / 8))
-        return fail(QPSK_ERR_ARGUMENT, "bits_stride_bytes smaller than 2*max_symbols/8");
-    if (syms && syms_stride_floats < 2 * max_sym)
-        return fail(QPSK_ERR_ARGUMENT, "syms_stride_floats smaller than 2*max_symbols");
+    Call c{mode, iq, stride_floats, n_samples, lengths, mem, bits, bits_stride_bytes, n_bits,
+           syms, syms_stride_floats, n_syms};
     int rc;
-    if (syms && !h->d_syms) {
-        if ((rc = dev_alloc(&h->d_syms, static_cast<size_t>(2 * S * h->syms_cap)))) return rc;
-    }
+    if ((rc = validate(h, c))) return rc;
+    const int S = h->S;
+    const int64_t n_call = c.n_call;
     hipStream_t st = h->stream;
     HIP_TRY(hipSetDevice(h->p.device));
-    hipEvent_t *ev = nullptr;
-    if (h->timing) {
-        if (h->ev_used == h->ev_pool.size()) {
-            std::array<hipEvent_t, 5> set{};
-            for (auto &e : set) HIP_TRY(hipEventCreate(&e));
-            h->ev_pool.push_back(set);
-        }
-        ev = h->ev_pool[h->ev_used++].data();
-        HIP_TRY(hipEventRecord(ev[0], st));
-    }
+    // pipelined calls issued before this one finish first (they share the state)
+    if (hipEvent_t e = last_async(h)) HIP_TRY(hipStreamWaitEvent(st, e, 0));
+    hipEvent_t *ev = next_events(h, &rc);
+    if (rc) return rc;
+    EV(0, st);
 
     // ---- input -----------------------------------------------------------
     const float *x = iq;
@@ -357,81 +571,98 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
                                  2 * n_call * sizeof(float), S, hipMemcpyHostToDevice, st));
         x = h->d_in;
         x_stride = h->n_max;
-    } else if (n_call > 0 && (stride_floats & 1)) {
-        return fail(QPSK_ERR_ARGUMENT, "device stride_floats must be even");
     }
     const int64_t *d_len = nullptr;
     if (lengths) {
-        HIP_TRY(hipMemcpyAsync(h->d_lengths, lengths, S * sizeof(int64_t), hipMemcpyHostToDevice, st));
-        d_len = h->d_lengths;
+        HIP_TRY(hipMemcpyAsync(h->d_lengths[0], lengths, S * sizeof(int64_t), hipMemcpyHostToDevice, st));
+        d_len = h->d_lengths[0];
     }
 
-    // ---- FLL (Band-Edge Filter.cs:64-87), README order FLL -> MF ------------
     if (h->p.enable_fll && n_call > 0) {
-        FllArgs fa{};
-        fa.x = x; fa.x_stride = x_stride;
-        fa.y = h->d_fll_out; fa.y_stride = h->n_max;
-        fa.delay = h->d_fll_delay;
-        fa.lengths = d_len; fa.n = n_call;
-        fa.state = h->d_state; fa.S = S;
-        launch_fll(fa, h->fp, st);
-        x = h->d_fll_out;
+        run_fll(h, x, x_stride, d_len, n_call, h->d_fll_out[0], st);
+        x = h->d_fll_out[0];
         x_stride = h->n_max;
     }
-    if (ev) HIP_TRY(hipEventRecord(ev[1], st));
+    EV(1, st);
+    if ((rc = run_fir(h, x, x_stride, d_len, n_call, h->d_mf[0], st, ev))) return rc;
+    return run_loop(h, c, d_len, h->d_mf[0], st, ev);
+}
 
-    // ---- matched filter (QPSKDeModulator.cs:360) ----------------------------
-    FirArgs fa{};
-    fa.x = x; fa.x_stride = x_stride;
-    fa.hist = h->d_hist[h->hist_cur];
-    fa.lengths = d_len; fa.n = n_call;
-    fa.y = h->d_mf; fa.y_stride = h->mf_stride; fa.y_offset = kMfPrefix;
-    if (n_call > 0) {
-        launch_fir(fa, h->taps, h->d_hrev, h->T, h->W, S, n_call, st);
-        if (ev) HIP_TRY(hipEventRecord(ev[2], st));
-        launch_fir_hist(fa, h->d_hist[h->hist_cur ^ 1], h->T - 1, S, st);
-        h->hist_cur ^= 1;
+int qpsk_demod_process_async(qpsk_demod *h, int32_t mode, const float *iq, int64_t stride_floats,
+                             int64_t n_samples, const int64_t *lengths, uint8_t *bits,
+                             int64_t bits_stride_bytes, int64_t *n_bits, float *syms,
+                             int64_t syms_stride_floats, int64_t *n_syms) {
+    Call c{mode, iq, stride_floats, n_samples, lengths, QPSK_MEM_DEVICE, bits, bits_stride_bytes,
+           n_bits, syms, syms_stride_floats, n_syms};
+    int rc;
+    if ((rc = validate(h, c))) return rc;
+    HIP_TRY(hipSetDevice(h->p.device));
+    if ((rc = pipe_setup(h))) return rc;
+    const int S = h->S;
+    const int64_t n_call = c.n_call;
+    const int b = h->pipe_bufs == 2 ? h->pipe_cur : 0;
+    h->pipe_cur ^= 1;
+    hipStream_t F = h->s_front, B = h->s_back;
+
+    // the front stage starts after the work already on the handle's stream
+    // (the producer of iq, earlier synchronous calls) and after the back stage
+    // that last used boundary buffer b
+    HIP_TRY(hipEventRecord(h->e_in, h->stream));
+    HIP_TRY(hipStreamWaitEvent(F, h->e_in, 0));
+    const int prev = h->pipe_bufs == 2 ? b : h->last_back;
+    if (prev >= 0 && h->back_rec[prev]) HIP_TRY(hipStreamWaitEvent(F, h->e_back[prev], 0));
+    hipEvent_t *ev = next_events(h, &rc);
+    if (rc) return rc;
+    const int64_t *d_len = nullptr;
+    if (lengths) {
+        // pinned staging row b is free once the front stage that last read it ran
+        if (h->front_rec[b]) HIP_TRY(hipEventSynchronize(h->e_front[b]));
+        std::memcpy(h->h_len[b], lengths, S * sizeof(int64_t));
+        HIP_TRY(hipMemcpyAsync(h->d_lengths[b], h->h_len[b], S * sizeof(int64_t), hipMemcpyHostToDevice, F));
+        d_len = h->d_lengths[b];
     }
-    if (ev && n_call <= 0) HIP_TRY(hipEventRecord(ev[2], st));
-    if (ev) HIP_TRY(hipEventRecord(ev[3], st));
-
-    // ---- symbol sync + Costas + decode (QPSKDeModulator.cs:364-408) --------
-    LoopArgs la{};
-    la.mf = h->d_mf; la.mf_stride = h->mf_stride;
-    la.carry = h->d_carry;
-    la.lengths = d_len; la.n = n_call;
-    la.state = h->d_state;
-    la.bits = mode == QPSK_MODE_DEMODULATE ? h->d_bits : nullptr;
-    la.bits_stride_words = h->bits_words;
-    la.bits_cap_words = h->bits_words;
-    la.n_bits = h->d_counts;
-    la.syms = syms ? h->d_syms : nullptr;
-    la.syms_stride = h->syms_cap;
-    la.syms_cap = h->syms_cap;
-    la.n_syms = h->d_counts + S;
-    la.S = S;
-    launch_loop(la, h->lp, mode, h->loop_variant, st);
-    HIP_TRY(hipGetLastError());
-    if (ev) HIP_TRY(hipEventRecord(ev[4], st));
-
-    // ---- outputs -----------------------------------------------------------
-    const hipMemcpyKind kind = mem == QPSK_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
-    const int64_t bytes_row = (2 * max_sym + 7) / 8;
-    if (bits && bytes_row > 0)
-        HIP_TRY(hipMemcpy2DAsync(bits, bits_stride_bytes, h->d_bits, h->bits_words * 4, bytes_row, S, kind, st));
-    if (syms && max_sym > 0)
-        HIP_TRY(hipMemcpy2DAsync(syms, syms_stride_floats * sizeof(float), h->d_syms,
-                                 2 * h->syms_cap * sizeof(float), 2 * max_sym * sizeof(float), S, kind, st));
-    if (mem == QPSK_MEM_HOST) {
-        HIP_TRY(hipMemcpyAsync(h->h_counts, h->d_counts, 2 * S * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        if (n_bits) std::memcpy(n_bits, h->h_counts, S * sizeof(int64_t));
-        if (n_syms) std::memcpy(n_syms, h->h_counts + S, S * sizeof(int64_t));
+    EV(0, F);
+    const float *x = iq;
+    const int64_t x_stride = stride_floats / 2;
+    float *mf;
+    if (h->p.enable_fll) {
+        // front = FLL into boundary rows b; back = FIR (MF rows 0) + loop
+        if (n_call > 0) run_fll(h, x, x_stride, d_len, n_call, h->d_fll_out[b], F);
+        EV(1, F);
+        HIP_TRY(hipEventRecord(h->e_front[b], F));
+        HIP_TRY(hipStreamWaitEvent(B, h->e_front[b], 0));
+        mf = h->d_mf[0];
+        if ((rc = run_fir(h, n_call > 0 ? h->d_fll_out[b] : x, n_call > 0 ? h->n_max : x_stride, d_len,
+                          n_call, mf, B, ev)))
+            return rc;
     } else {
-        if (n_bits) HIP_TRY(hipMemcpyAsync(n_bits, h->d_counts, S * sizeof(int64_t), kind, st));
-        if (n_syms) HIP_TRY(hipMemcpyAsync(n_syms, h->d_counts + S, S * sizeof(int64_t), kind, st));
+        // front = FIR into MF rows b; back = loop
+        EV(1, F);
+        mf = h->d_mf[b];
+        if ((rc = run_fir(h, x, x_stride, d_len, n_call, mf, F, ev))) return rc;
+        HIP_TRY(hipEventRecord(h->e_front[b], F));
+        HIP_TRY(hipStreamWaitEvent(B, h->e_front[b], 0));
     }
+    h->front_rec[b] = true;
+    if ((rc = run_loop(h, c, d_len, mf, B, ev))) return rc;
+    HIP_TRY(hipEventRecord(h->e_back[b], B));
+    h->back_rec[b] = true;
+    h->last_back = b;
     return QPSK_OK;
+}
+
+int qpsk_demod_pipeline_wait(qpsk_demod *h, void *hip_stream) {
+    if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
+    hipEvent_t e = last_async(h);
+    if (!e) return QPSK_OK;
+    if (hip_stream) HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(hip_stream), e, 0));
+    else HIP_TRY(hipEventSynchronize(e));
+    return QPSK_OK;
+}
+
+int qpsk_demod_pipeline_depth(const qpsk_demod *h) {
+    if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
+    return h->pipe_ready ? h->pipe_bufs : 0;
 }
 
 int qpsk_demod_rrc_taps(const qpsk_demod *h, float *taps, int32_t cap) {
@@ -494,6 +725,8 @@ int qpsk_demod_get_state(const qpsk_demod *h, void *host_buf) {
     if (!h || !host_buf) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
     const int64_t S = h->S, H = h->T - 1;
     char *p = static_cast<char *>(host_buf);
+    int rc;
+    if ((rc = drain_async(h))) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
     HIP_TRY(hipMemcpy(p, h->d_state, S * sizeof(StreamState), hipMemcpyDeviceToHost));
     p += S * sizeof(StreamState);
@@ -509,6 +742,8 @@ int qpsk_demod_set_state(qpsk_demod *h, const void *host_buf) {
     if (!h || !host_buf) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
     const int64_t S = h->S, H = h->T - 1;
     const char *p = static_cast<const char *>(host_buf);
+    int rc;
+    if ((rc = drain_async(h))) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
     HIP_TRY(hipMemcpy(h->d_state, p, S * sizeof(StreamState), hipMemcpyHostToDevice));
     p += S * sizeof(StreamState);

@@ -259,6 +259,85 @@ def test_synth_generated_batch_parity_and_ber():
     assert clean >= S // 2
 
 
+def async_run(iq2d, calls, sps, span, sync_every=0, **kw):
+    """The same call sequence through qpsk_demod_process_async (front stage of
+    call k+1 overlapping the back stage of call k), every call's outputs in
+    their own device rows, one pipeline_wait at the end.  sync_every > 0 makes
+    every sync_every-th call a synchronous process() (mixed ordering)."""
+    import torch
+    S = iq2d.shape[0]
+    nmax = max(max(c) for c in calls)
+    p = Q.params(K.FS, K.FS // sps, K.ALPHA, span, max_samples_per_call=nmax + 8, **kw)
+    b = Q.BatchDemodulator(S, p)
+    stream = torch.cuda.Stream()
+    b.set_stream(stream.cuda_stream)
+    ms = max(b.max_symbols(nmax), 1)
+    pos = np.zeros(S, dtype=np.int64)
+    outs = []
+    with torch.cuda.stream(stream):
+        for ci, lens in enumerate(calls):
+            n = int(max(lens))
+            x = np.zeros((S, 2 * max(n, 1)), np.float32)
+            for s in range(S):
+                x[s, : 2 * lens[s]] = iq2d[s, 2 * pos[s]: 2 * (pos[s] + lens[s])]
+            xd = torch.from_numpy(x).to("cuda", non_blocking=False)
+            bits = torch.zeros((S, (2 * ms + 7) // 8 + 8), dtype=torch.uint8, device="cuda")
+            nb = torch.zeros(S, dtype=torch.int64, device="cuda")
+            sy = torch.zeros((S, 2 * ms), dtype=torch.float32, device="cuda")
+            ns = torch.zeros(S, dtype=torch.int64, device="cuda")
+            uniform = all(l == lens[0] for l in lens)
+            if sync_every and ci % sync_every == sync_every - 1:
+                assert uniform
+                b.process_device(xd, n, bits, nb, syms_dev=sy, n_syms_dev=ns)
+            else:
+                b.process_device_async(xd, n, bits, nb, syms_dev=sy, n_syms_dev=ns,
+                                       lengths=None if uniform else np.array(lens))
+            outs.append((xd, bits, nb, sy, ns))
+            pos += np.array(lens)
+    depth = b.pipeline_depth()
+    b.pipeline_wait()
+    torch.cuda.synchronize()
+    res = []
+    for _, bits, nb, sy, ns in outs:
+        bits, nb, sy, ns = bits.cpu().numpy(), nb.cpu().numpy(), sy.cpu().numpy(), ns.cpu().numpy()
+        res.append([(Q.unpack_bits(bits[s], int(nb[s])), sy[s, : 2 * int(ns[s])].copy()) for s in range(S)])
+    b.close()
+    return res, depth
+
+
+@pytest.mark.parametrize("fll", [False, True])
+def test_pipelined_calls_bit_exact(fll):
+    """qpsk_demod_process_async: uniform and ragged calls, empty calls, with and
+    without the FLL (whose front stage is the FLL instead of the FIR)."""
+    kw = dict(enable_fll=True, cfo_loop_bandwidth=1e-3) if fll else {}
+    okw = dict(enable_fll=True, cfo_loop_bw=1e-3) if fll else {}
+    iq = K.batch_signals(5, seed0=400, sps=8, span=8, n_bits=2400, snr_db=16,
+                         cfo_hz=3000.0 if fll else 0.0)
+    n = iq.shape[1] // 2
+    rng = np.random.default_rng(11)
+    calls, used = [], np.zeros(5, np.int64)
+    for c in range(7):
+        lens = np.full(5, 1500) if c % 3 == 0 else rng.integers(0, 2500, 5)
+        if c == 4:
+            lens[:] = 0
+        calls.append([int(v) for v in lens])
+        used += lens
+    calls.append([int(n - u) for u in used])
+    got, depth = async_run(iq, calls, 8, 8, **kw)
+    assert depth == 2
+    assert_same(got, oracle_run(iq, calls, 8, 8, **okw))
+
+
+def test_pipelined_mixed_with_sync_calls():
+    """Synchronous process() calls interleaved with pipelined ones keep one order."""
+    iq = K.batch_signals(3, seed0=410, sps=4, span=32, n_bits=3000, snr_db=16)
+    n = iq.shape[1] // 2
+    k = n // 6
+    calls = [[k] * 3 for _ in range(5)] + [[n - 5 * k] * 3]
+    got, _ = async_run(iq, calls, 4, 32, sync_every=2)
+    assert_same(got, oracle_run(iq, calls, 4, 32))
+
+
 def test_huge_amplitude_takes_the_costas_rollback_path():
     """Samples scaled by 1e12 drive theta far past the table reduction's range
     (|theta| > 1e6): the loop kernel's fast pass detects it and redoes the round
