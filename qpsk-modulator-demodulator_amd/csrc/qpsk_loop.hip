@@ -90,9 +90,6 @@ __device__ __forceinline__ sym_t to_sym(float, float, double cid, double cqd) { 
 __device__ __forceinline__ d2 from_sym(d2 v) { return v; }
 __device__ __forceinline__ f2 sym_to_f2(d2 v) { return f2{static_cast<float>(v.x), static_cast<float>(v.y)}; }
 #endif
-#ifndef QPSK_LOOP_PRIO
-#define QPSK_LOOP_PRIO 3
-#endif
 
 __device__ __forceinline__ int wave_max_i32(int v) {
 #pragma unroll
@@ -148,10 +145,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     const int lane = threadIdx.x & 63;
     const int s = blockIdx.x * SPW + lane;
     const bool valid = lane < SPW && s < a.S;
-    // every wave here runs a latency-bound chain: should a pipelined call's
-    // front-stage workgroups share a SIMD with them, these waves win VALU
-    // arbitration
-    __builtin_amdgcn_s_setprio(QPSK_LOOP_PRIO);
 
     // ---- per-stream queue geometry (every wave: lane l <-> stream blk*SPW + l)
     int n = 0, cnt = 0, R = 0, d = 0;
