@@ -80,12 +80,12 @@ def load_traffic(config_key: str):
         return None
 
 
-def cpu_baseline(host_iq, sps, span, n_threads):
+def cpu_baseline(host_iq, sps, span, n_threads, fll=False):
     import numpy as np
     import oracle as O
     t0 = time.perf_counter()
     nb = O.demod_batch_timed(host_iq, FS, FS // sps, n_threads=n_threads, rrc_alpha=ALPHA,
-                             rrc_span=span, trig=O.TRIG_LIBM)
+                             rrc_span=span, trig=O.TRIG_LIBM, enable_fll=fll)
     dt = time.perf_counter() - t0
     S, nf = host_iq.shape
     return S * (nf // 2) / dt / 1e6, dt, int(np.sum(nb))
@@ -379,11 +379,12 @@ def main():
         host = iq[:ns].cpu().numpy()
         ncpu = os.cpu_count() or 1
         threads = args.cpu_threads or max(1, min(16, ncpu))
-        v, dt, _ = cpu_baseline(host, sps, span, threads)
+        v, dt, _ = cpu_baseline(host, sps, span, threads, fll=cfg["fll"])
         what = f"full {args.config} batch" if ns == S else f"first {ns} of {S} {args.config} streams"
         cpu = {"value": round(v, 2), "unit": "MSa/s", "cores": threads, "kind": "port",
                "sample": f"{what} ({ns} streams x {n} samples) on {threads} host threads, "
-                         f"one oracle demodulator (glibc trig) per stream, {dt:.2f} s wall"}
+                         f"one oracle demodulator (glibc trig{', FLL on' if cfg['fll'] else ''}) per stream, "
+                         f"{dt:.2f} s wall"}
 
     samples_total = world * S * n * args.steps
     value = samples_total / t_max / 1e6
