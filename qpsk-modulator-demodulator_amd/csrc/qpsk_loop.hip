@@ -55,6 +55,12 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 // sample ring holds 4 rounds (index = p & (4*KB - 1)), preceded by a mirror of
 // its last 4 samples so the 4 interpolation taps are always contiguous in LDS.
 constexpr int kMir = 4;
+#ifndef QPSK_COSTAS_UNROLL2
+#define QPSK_COSTAS_UNROLL2 1
+#endif
+#ifndef QPSK_MM_LSHLADD
+#define QPSK_MM_LSHLADD 1
+#endif
 #ifndef QPSK_RING_PAD
 #define QPSK_RING_PAD 0
 #endif
@@ -295,7 +301,15 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         auto taps_fl = [&](double fl) -> lds_f2 * {
             union { double v; unsigned long long u; } kb;
             kb.v = fl + tap_shift;
+#if QPSK_MM_LSHLADD
+            // and + lshl_add: one op shorter than the shift, and, add the
+            // compiler canonicalises 8 * (i & m) + base into
+            const uint32_t idx = static_cast<uint32_t>(kb.u) & (kRing - 1);
+            uint32_t addr;
+            asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(addr) : "v"(idx), "v"(tap0));
+#else
             const uint32_t addr = tap0 + 8u * (static_cast<uint32_t>(kb.u) & (kRing - 1));
+#endif
             return reinterpret_cast<lds_f2 *>(static_cast<uintptr_t>(addr));
         };
         // symbols that start in every 64-sample round once a stream is inside its
@@ -620,12 +634,29 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             double amax = fabs(theta);   // largest sincos argument of the round
             STAMP(tu);
             if (m >= mlo) {              // every stream the M&M ran uniformly
+                // one v_max_f64 (fmax would first canonicalize amax)
+                auto track = [&]() { asm volatile("v_max_f64 %0, %0, |%1|" : "+v"(amax) : "v"(theta)); };
+#if QPSK_COSTAS_UNROLL2
+                // by two: y and the next symbol alternate registers instead of
+                // being copied back every symbol
+                for (; k + 1 < mlo; k += 2) {   // uniform trip count
+                    step(k, std::false_type{});
+                    track();
+                    step(k + 1, std::false_type{});
+                    track();
+                }
+                if (k < mlo) {
+                    step(k, std::false_type{});
+                    track();
+                    ++k;
+                }
+#else
 #pragma unroll 4
                 for (; k < mlo; ++k) {   // uniform trip count
                     step(k, std::false_type{});
-                    // one v_max_f64 (fmax would first canonicalize amax)
-                    asm volatile("v_max_f64 %0, %0, |%1|" : "+v"(amax) : "v"(theta));
+                    track();
                 }
+#endif
             }
             ACC(k_uni, tu);
 #ifdef QPSK_LOOP_STAMPS
