@@ -219,6 +219,47 @@ def split_gather(demod, fresh_state, iq_local, bits, nbits, S, n, world, rank, d
 TSC_BITS = "11001010011101100100100110101100" + "01110100111001011010001101101001"  # testAtDataLevel.cs:20-22
 
 
+def host_ring_pass(demod, iq, S, n, steps=6, warmup=2, depth=2):
+    """PCIe-inclusive rate of the host-fed streaming front-end (qpsk_rx_*, the
+    ModDemodOverSDR.cs:116-183 receive loop): every call uploads S x n samples
+    from pinned host slots while the previous call computes.  Untimed set-up:
+    the synthetic batch is copied once into each pinned slot, which later
+    submits reuse in place (an SDR driver would DMA into them)."""
+    import qpsk_amd as Q
+    host = iq.cpu().numpy()
+    ring = Q.HostRing(demod, depth)
+    pending = 0
+
+    def submit():
+        nonlocal pending
+        if pending == depth:
+            ring.collect()
+            pending -= 1
+        ring.submit(None, n)
+        pending += 1
+
+    for _ in range(depth):                 # fill every slot once
+        ring.next_slot()[:, : 2 * n] = host[:, : 2 * n]
+        submit()
+    for _ in range(warmup):
+        submit()
+    while pending:
+        ring.collect()
+        pending -= 1
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        submit()
+    while pending:
+        ring.collect()
+        pending -= 1
+    dt = time.perf_counter() - t0
+    ring.close()
+    return {"value": round(S * n * steps / dt / 1e6, 2), "unit": "MSa/s",
+            "ms_per_call": round(dt / steps * 1e3, 3), "depth": depth, "steps": steps,
+            "h2d_GBps": round(8.0 * S * n * steps / dt / 1e9, 2),
+            "note": "host pinned slots -> H2D -> demod -> D2H bits, calls overlapped; not the headline value"}
+
+
 def framer_pass(bits, nbits, S, stream, reps=5):
     """§8f rank 1, measured beside the headline (never inside it): the device
     TSC search + DeModulateBytes framer over the bit rows the chain just
@@ -266,6 +307,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo + --share-gpu rehearses the N>1 path on a one-GPU box")
+    ap.add_argument("--no-host-ring", action="store_true",
+                    help="skip the PCIe-inclusive host-ring pass (run at N=1 for batches <= 4 GiB)")
     ap.add_argument("--no-framer", action="store_true",
                     help="skip the device TSC + framer pass measured beside the headline")
     ap.add_argument("--no-split-gather", action="store_true",
@@ -432,6 +475,8 @@ def main():
         out["framer"] = fr_stats
     if sg is not None:
         out["split_gather"] = sg
+    if world == 1 and not args.no_host_ring and S * n * 8 <= (4 << 30):
+        out["host_ring"] = host_ring_pass(demod, iq, S, n)
     if rank == 0:
         print(json.dumps(out), flush=True)
     demod.close()

@@ -163,6 +163,43 @@ int qpsk_demod_get_state(const qpsk_demod *h, void *host_buf);
 int qpsk_demod_set_state(qpsk_demod *h, const void *host_buf);
 
 /* ---------------------------------------------------------------------------
+ * Host-fed streaming front-end: the deployment shape of
+ * ModDemodOverSDR.cs:116-183, where the SDR thread hands CF32 buffers to
+ * DeModulate one after another.  A ring of `depth` pinned host slots feeds one
+ * handle: submit k uploads slot k on the DMA engine and queues a pipelined
+ * DeModulate of it (qpsk_demod_process_async), so chunk k+1's upload overlaps
+ * chunk k's matched filter and symbol loop, and chunk k's bits come back while
+ * chunk k+1 computes.  collect returns the oldest outstanding chunk's bits.
+ * Results equal consecutive qpsk_demod_process calls on the same chunks.  One
+ * caller thread per ring, as for the handle (QPSKDeModulator is not
+ * thread-safe either).
+ */
+typedef struct qpsk_rx qpsk_rx;
+/* depth: 2..8 slots of n_streams x max_samples_per_call complex samples.  The
+ * ring binds the handle to its own upload stream (as qpsk_demod_set_stream);
+ * do not call the handle directly while the ring lives. */
+int qpsk_rx_create(qpsk_demod *h, int32_t depth, qpsk_rx **out);
+/* Waits for every outstanding chunk, then frees the ring (the handle keeps its
+ * state and returns to a library-owned stream). */
+int qpsk_rx_destroy(qpsk_rx *r);
+/* The pinned host slot the next submit reads, [n_streams][*stride_floats]
+ * interleaved I,Q: fill it in place (e.g. as an SDR driver's receive buffer)
+ * and pass it to submit to skip the host copy.  QPSK_ERR_STATE while that slot
+ * still holds an uncollected chunk. */
+int qpsk_rx_next_slot(qpsk_rx *r, float **iq, int64_t *stride_floats);
+/* Queue one DeModulate call on every stream.  iq: host rows, copied into the
+ * slot unless iq is the slot itself; n_samples / lengths as in
+ * qpsk_demod_process.  *ticket = the call's sequence number (may be NULL).
+ * QPSK_ERR_STATE when all depth slots hold uncollected chunks. */
+int qpsk_rx_submit(qpsk_rx *r, const float *iq, int64_t stride_floats, int64_t n_samples,
+                   const int64_t *lengths, int64_t *ticket);
+/* Wait for the oldest uncollected chunk and copy its bits (packed MSB-first,
+ * as qpsk_demod_process) and bit counts to host memory.  QPSK_ERR_STATE when
+ * nothing is outstanding. */
+int qpsk_rx_collect(qpsk_rx *r, uint8_t *bits, int64_t bits_stride_bytes, int64_t *n_bits,
+                    int64_t *ticket);
+
+/* ---------------------------------------------------------------------------
  * Byte framer (DeModulateBytes, QPSKDeModulator.cs:169-259), batched: one
  * framer per stream fed with the packed bits of each process() call.
  */

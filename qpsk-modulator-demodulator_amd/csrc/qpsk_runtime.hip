@@ -126,6 +126,15 @@ struct qpsk_demod {
     int64_t *h_len[2] = {nullptr, nullptr};   // pinned staging of per-call lengths
 };
 
+namespace qpsk {
+// the pipelined path's front-stage stream (qpsk_rx.hip records "input consumed"
+// on it); nullptr before the first pipelined call
+hipStream_t pipe_front_stream(const qpsk_demod *h) { return h->s_front; }
+int handle_streams(const qpsk_demod *h) { return h->S; }
+int64_t handle_max_samples(const qpsk_demod *h) { return h->n_max; }
+int handle_device(const qpsk_demod *h) { return h->p.device; }
+}  // namespace qpsk
+
 namespace {
 
 // The newest pipelined call's back stage, or nullptr.

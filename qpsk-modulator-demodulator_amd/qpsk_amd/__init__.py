@@ -164,6 +164,12 @@ def lib():
     L.qpsk_synth_params_init.argtypes = [C.POINTER(SynthParams), C.c_int32, C.c_int32]
     L.qpsk_synth_generate.argtypes = [C.POINTER(SynthParams), C.c_int32, C.c_void_p, C.c_int32,
                                       C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]
+    L.qpsk_rx_create.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]
+    L.qpsk_rx_destroy.argtypes = [C.c_void_p]
+    L.qpsk_rx_next_slot.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
+    L.qpsk_rx_submit.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, _i64p,
+                                 C.POINTER(C.c_int64)]
+    L.qpsk_rx_collect.argtypes = [C.c_void_p, _u8p, C.c_int64, _i64p, C.POINTER(C.c_int64)]
     _lib = real
     return real
 
@@ -178,7 +184,8 @@ EXPORTED_SYMBOLS = [
     "qpsk_framer_dev_destroy", "qpsk_framer_dev_set_stream", "qpsk_framer_dev_set_markers",
     "qpsk_framer_dev_push", "qpsk_framer_dev_status", "qpsk_tsc_find_device",
     "qpsk_synth_params_init", "qpsk_synth_generate", "qpsk_demod_process_async",
-    "qpsk_demod_pipeline_wait", "qpsk_demod_pipeline_depth",
+    "qpsk_demod_pipeline_wait", "qpsk_demod_pipeline_depth", "qpsk_rx_create", "qpsk_rx_destroy",
+    "qpsk_rx_next_slot", "qpsk_rx_submit", "qpsk_rx_collect",
 ]
 
 _EXC = {
@@ -358,6 +365,66 @@ class BatchDemodulator:
 
     def pipeline_depth(self) -> int:
         return _check(lib().qpsk_demod_pipeline_depth(self._h))
+
+
+class HostRing:
+    """Host-fed streaming front-end over one BatchDemodulator (qpsk_rx_*, the
+    ModDemodOverSDR.cs:116-183 receive loop): submit() queues one DeModulate call
+    on host samples, collect() returns the oldest outstanding call's bits.  The
+    handle must not be used directly while the ring lives."""
+
+    def __init__(self, demod: "BatchDemodulator", depth: int = 2):
+        self._demod = demod
+        self.S = demod.S
+        self._r = C.c_void_p()
+        _check(lib().qpsk_rx_create(demod._h, int(depth), C.byref(self._r)))
+        ms = demod.max_symbols(int(demod.p.max_samples_per_call))
+        self.bits_stride = (2 * ms + 7) // 8
+
+    def next_slot(self) -> np.ndarray:
+        """The pinned slot the next submit reads, as a writable (S, stride) float32 view."""
+        ptr, stride = C.c_void_p(), C.c_int64()
+        _check(lib().qpsk_rx_next_slot(self._r, C.byref(ptr), C.byref(stride)))
+        buf = (C.c_float * (self.S * stride.value)).from_address(ptr.value)
+        return np.ctypeslib.as_array(buf).reshape(self.S, stride.value)
+
+    def submit(self, iq: np.ndarray | None = None, n: int | None = None, lengths=None) -> int:
+        """iq None: the slot from next_slot() (filled in place); else (S, >= 2n) float32 rows."""
+        if iq is None:
+            slot = self.next_slot()
+            ptr, stride = slot.ctypes.data, slot.shape[1]
+        else:
+            iq = np.ascontiguousarray(iq, dtype=np.float32)
+            assert iq.shape[0] == self.S
+            ptr, stride = iq.ctypes.data, iq.shape[1]
+        if n is None:
+            n = stride // 2
+        lens = None if lengths is None else np.ascontiguousarray(lengths, dtype=np.int64)
+        t = C.c_int64()
+        _check(lib().qpsk_rx_submit(self._r, C.c_void_p(ptr), int(stride), int(n),
+                                    lens.ctypes.data_as(_i64p) if lens is not None else None,
+                                    C.byref(t)))
+        return t.value
+
+    def collect(self):
+        """(bits (S, stride) uint8, n_bits (S,) int64, ticket) of the oldest outstanding call."""
+        bits = np.zeros((self.S, self.bits_stride), dtype=np.uint8)
+        nb = np.zeros(self.S, dtype=np.int64)
+        t = C.c_int64()
+        _check(lib().qpsk_rx_collect(self._r, bits.ctypes.data_as(_u8p), self.bits_stride,
+                                     nb.ctypes.data_as(_i64p), C.byref(t)))
+        return bits, nb, t.value
+
+    def close(self):
+        if self._r:
+            _check(lib().qpsk_rx_destroy(self._r))
+            self._r = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def design(p: DemodParams):

@@ -352,3 +352,92 @@ def test_huge_amplitude_takes_the_costas_rollback_path():
             assert np.array_equal(sa.view(np.uint32), sb.view(np.uint32)), f"call {ci} stream {s}"
     # (with |pe| ~ 1e12 the first symbol already moves freq by cb*pe ~ 1e10, so
     # theta leaves [-1e6, 1e6] within a round)
+
+
+def ring_run(iq2d, calls, sps, span, depth=2, zero_copy=False, **kw):
+    """The host-fed ring (qpsk_rx_*): submit every call, collecting only when the
+    ring is full, so uploads and computes of consecutive calls overlap."""
+    S = iq2d.shape[0]
+    p = Q.params(K.FS, K.FS // sps, K.ALPHA, span, max_samples_per_call=max(max(c) for c in calls) + 8, **kw)
+    b = Q.BatchDemodulator(S, p)
+    ring = Q.HostRing(b, depth)
+    pos = np.zeros(S, dtype=np.int64)
+    out, pending = [], 0
+
+    def collect():
+        bits, nb, _ = ring.collect()
+        out.append([(Q.unpack_bits(bits[s], int(nb[s])), None) for s in range(S)])
+
+    for lens in calls:
+        n = int(max(lens))
+        uniform = all(l == lens[0] for l in lens)
+        if pending == depth:
+            collect()
+            pending -= 1
+        if zero_copy:
+            slot = ring.next_slot()
+            for s in range(S):
+                slot[s, : 2 * lens[s]] = iq2d[s, 2 * pos[s]: 2 * (pos[s] + lens[s])]
+            ring.submit(None, n, None if uniform else np.array(lens))
+        else:
+            x = np.zeros((S, 2 * max(n, 1)), np.float32)
+            for s in range(S):
+                x[s, : 2 * lens[s]] = iq2d[s, 2 * pos[s]: 2 * (pos[s] + lens[s])]
+            ring.submit(x, n, None if uniform else np.array(lens))
+        pending += 1
+        pos += np.array(lens)
+    while pending:
+        collect()
+        pending -= 1
+    ring.close()
+    b.close()
+    return out
+
+
+def assert_same_bits(got, want):
+    for ci, (ra, rb) in enumerate(zip(got, want)):
+        for s, ((ba, _), (bb, _)) in enumerate(zip(ra, rb)):
+            assert ba == bb, f"call {ci} stream {s}: bits differ ({len(ba)} vs {len(bb)})"
+
+
+@pytest.mark.parametrize("depth,zero_copy,fll", [(2, False, False), (3, True, False), (2, True, True)])
+def test_host_ring_bit_exact(depth, zero_copy, fll):
+    """The streaming front-end (ModDemodOverSDR.cs:116-183 receive loop): uniform,
+    ragged and empty chunks through the pinned ring give the oracle's bits."""
+    kw = dict(enable_fll=True, cfo_loop_bandwidth=1e-3) if fll else {}
+    okw = dict(enable_fll=True, cfo_loop_bw=1e-3) if fll else {}
+    iq = K.batch_signals(4, seed0=500 + depth, sps=8, span=8, n_bits=2400, snr_db=16,
+                         cfo_hz=3000.0 if fll else 0.0)
+    n = iq.shape[1] // 2
+    rng = np.random.default_rng(21 + depth)
+    calls, used = [], np.zeros(4, np.int64)
+    for c in range(7):
+        lens = np.full(4, 1300) if c % 3 == 0 else rng.integers(0, 2200, 4)
+        if c == 5:
+            lens[:] = 0
+        calls.append([int(v) for v in lens])
+        used += lens
+    calls.append([int(n - u) for u in used])
+    got = ring_run(iq, calls, 8, 8, depth=depth, zero_copy=zero_copy, **kw)
+    assert_same_bits(got, oracle_run(iq, calls, 8, 8, **okw))
+
+
+def test_host_ring_errors():
+    p = Q.params(K.FS, K.FS // 8, K.ALPHA, 8, max_samples_per_call=4096)
+    b = Q.BatchDemodulator(2, p)
+    with pytest.raises(ValueError):
+        Q.HostRing(b, 1)
+    ring = Q.HostRing(b, 2)
+    with pytest.raises(Q.QPSKError):
+        ring.collect()                    # nothing outstanding
+    x = np.zeros((2, 2 * 1000), np.float32)
+    ring.submit(x, 1000)
+    ring.submit(x, 1000)
+    with pytest.raises(Q.QPSKError):
+        ring.submit(x, 1000)              # both slots hold uncollected chunks
+    ring.collect()
+    with pytest.raises(ValueError):
+        ring.submit(np.zeros((2, 2 * 5000), np.float32), 5000)   # > max_samples_per_call
+    ring.collect()
+    ring.close()
+    b.close()
