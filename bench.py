@@ -80,6 +80,16 @@ def load_traffic(config_key: str):
         return None
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(host_iq, sps, span, n_threads, fll=False):
     import numpy as np
     import oracle as O
@@ -423,11 +433,15 @@ def main():
         ncpu = os.cpu_count() or 1
         threads = args.cpu_threads or max(1, min(16, ncpu))
         v, dt, _ = cpu_baseline(host, sps, span, threads, fll=cfg["fll"])
+        # one core on the first 8 streams (single-core and all-core)
+        v1, dt1, _ = cpu_baseline(host[: min(ns, 8)], sps, span, 1, fll=cfg["fll"])
         what = f"full {args.config} batch" if ns == S else f"first {ns} of {S} {args.config} streams"
         cpu = {"value": round(v, 2), "unit": "MSa/s", "cores": threads, "kind": "port",
+               "single_core": round(v1, 2), "cpu_model": cpu_model(), "host_cpus": ncpu,
                "sample": f"{what} ({ns} streams x {n} samples) on {threads} host threads, "
                          f"one oracle demodulator (glibc trig{', FLL on' if cfg['fll'] else ''}) per stream, "
-                         f"{dt:.2f} s wall"}
+                         f"{dt:.2f} s wall; single_core: first {min(ns, 8)} streams on 1 thread, "
+                         f"{dt1:.2f} s wall"}
 
     samples_total = world * S * n * args.steps
     value = samples_total / t_max / 1e6
