@@ -509,7 +509,11 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                     return (base + 2 < rend) & (k < kmax) &
                            (last | (static_cast<double>(rend - d - 3) - nt >= lag_max));
                 };
+#if QPSK_MM_VOTE4
+                if (__builtin_amdgcn_ballot_w64(more()) != 0) {   // one vote skips the loop in steady state
+#else
                 if (__ballot(more()) != 0) {   // one vote skips the loop in steady state
+#endif
                     reload();                   // the uniform loop ended on a tap-less step
                     while (more()) step(std::true_type{});
                 }
