@@ -7,6 +7,32 @@
 #include <random>
 using namespace qpsk;
 
+// optional load beside the loop kernel (argv[4] = number of workgroups): one
+// FMA-bound workgroup per CU (100 KB LDS keeps it off the loop's CUs), run on
+// a second stream for ~2x the loop's time, to see whether the loop slows in
+// cycles (contention) or only in wall time (clock)
+// memory-bound variant: streams a large buffer (read + write) for the same time
+__global__ void burn_mem_kernel(const float4 *src, float4 *dst, long long n4, long long ticks) {
+  extern __shared__ float lds[];
+  if (threadIdx.x == 0) lds[0] = 0.f;
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) dst[i] = src[i];
+  }
+}
+__global__ void burn_kernel(float *sink, long long ticks) {
+  extern __shared__ float lds[];
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  float x = threadIdx.x, y = blockIdx.x;
+  if (threadIdx.x == 0) lds[0] = x;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+#pragma unroll 32
+    for (int i = 0; i < 256; ++i) { x = x * 1.0000001f + 1e-7f; y = y * 0.9999999f + 1e-7f; }
+  }
+  if (x + y == 12345.0f) sink[threadIdx.x] = x;
+}
+
 int main(int argc, char** argv) {
   const int S = argc > 1 ? atoi(argv[1]) : 256;
   const int64_t n = argc > 2 ? atoll(argv[2]) : (1 << 20);
@@ -27,13 +53,37 @@ int main(int argc, char** argv) {
   a.bits_stride_words = words; a.bits_cap_words = words; a.n_bits = cnt; a.n_syms = cnt + S; a.S = S; a.probe = probe;
   LoopParams P{}; P.sps = 8.0; P.kp = 2.622462326512427e-3; P.ki = 3.443172085385801e-06; P.c_alpha = 0.13751550967894244; P.c_beta = 0.010184293139132996; P.differential = 1;
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+  const int burn = argc > 4 ? atoi(argv[4]) : 0;
+  hipStream_t bs; hipStreamCreateWithFlags(&bs, hipStreamNonBlocking);
+  float *sink; hipMalloc(&sink, 4096);
+  const int burn_mem = argc > 5 ? atoi(argv[5]) : 0;
+  float4 *bsrc = nullptr, *bdst = nullptr;
+  const long long bn4 = (1LL << 30) / 16;   // 1 GiB each way
+  if (burn > 0 && burn_mem) { hipMalloc(&bsrc, bn4 * 16); hipMalloc(&bdst, bn4 * 16); hipMemset(bsrc, 0, bn4 * 16); }
+  auto burn_launch = [&]() {
+    if (burn_mem) {
+      hipFuncSetAttribute((const void *)burn_mem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 100 << 10);
+      hipLaunchKernelGGL(burn_mem_kernel, dim3(burn), dim3(1024), 100 << 10, bs, bsrc, bdst, bn4, 6000000LL);
+    } else {
+      hipFuncSetAttribute((const void *)burn_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 100 << 10);
+      hipLaunchKernelGGL(burn_kernel, dim3(burn), dim3(256), 100 << 10, bs, sink, 6000000LL);   // 60 ms
+    }
+  };
+  if (burn > 0) {
+    burn_launch();
+    hipDeviceSynchronize();   // warm: let the clock settle under the load once
+    burn_launch();
+  }
+  const long long rt0 = 0; (void)rt0;
   hipEventRecord(e0);
   launch_loop(a, P, kModeDemodulate, spw, 0);
   hipEventRecord(e1); hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
   std::vector<unsigned long long> pr(16 * S); hipMemcpy(pr.data(), probe, pr.size() * 8, hipMemcpyDeviceToHost);
   int64_t ns; hipMemcpy(&ns, cnt + S, 8, hipMemcpyDeviceToHost);
-  printf("S=%d n=%lld variant=%d: %.3f ms, stream0 symbols %lld -> %.1f ns/symbol\n", S, (long long)n, spw, ms, (long long)ns, ms * 1e6 / ns);
+  printf("S=%d n=%lld variant=%d burn=%d: %.3f ms, stream0 symbols %lld -> %.1f ns/symbol, WG0 M&M cycles %.3g -> %.2f GHz effective\n",
+         S, (long long)n, spw, burn, ms, (long long)ns, ms * 1e6 / ns, (double)(pr[2] + pr[3]),
+         (double)(pr[2] + pr[3]) / (ms * 1e6));
   const int nwg = (int)((S + (spw == 0 || spw == 2 ? 32 : 16) - 1) / (spw == 0 || spw == 2 ? 32 : 16));
   for (int b = 0; b < nwg; ++b) {
     auto* p = &pr[16 * b];
