@@ -61,12 +61,7 @@ constexpr int kMir = 4;
 #ifndef QPSK_MM_LSHLADD
 #define QPSK_MM_LSHLADD 1
 #endif
-#ifndef QPSK_MM_VOTE4
-#define QPSK_MM_VOTE4 1
-#endif
-#ifndef QPSK_MM_FIRST_SKIP
-#define QPSK_MM_FIRST_SKIP 0   // A/B: 24.6 ms with it, 24.1 without (C2 loop; with VOTE4 25.1)
-#endif
+
 #ifndef QPSK_RING_PAD
 #define QPSK_RING_PAD 0
 #endif
@@ -335,9 +330,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         // exact sum as the reference's (double)d1*x1 + (double)d2*x2
         double psid = psi, psqd = psq;
         double pdid = pdi >= 0.0f ? 1.0 : -1.0, pdqd = pdq >= 0.0f ? 1.0 : -1.0;
-#if QPSK_MM_FIRST_SKIP
-        bool any_first = __builtin_amdgcn_ballot_w64(!has_prev) != 0;   // wave-uniform
-#endif
 #ifdef QPSK_LOOP_STAMPS
         unsigned long long c_bar = 0, c_loop = 0, c_iters = 0, c_uni = 0, c_uit = 0, c_pre = 0, c_post = 0;
 #endif
@@ -395,12 +387,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 tp = (lds_f2 *)taps(base);
                 xm1 = tp[0]; x0 = tp[1]; x1 = tp[2]; x2 = tp[3];
             };
-#if QPSK_MM_FIRST_SKIP
-            // once every stream has its first symbol, one scalar test skips this
-            if (any_first && !has_prev && base + 2 < rend && kmax > 0) {
-#else
             if (!has_prev && base + 2 < rend && kmax > 0) {
-#endif
                 // very first symbol of the stream: no TED, advance = sps (MuellerMuller.cs:93-97)
                 float ci, cq;
                 interp(ci, cq);
@@ -412,9 +399,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 pdqd = cq >= 0.0f ? 1.0 : -1.0;
                 advance(sps, std::true_type{});
             }
-#if QPSK_MM_FIRST_SKIP
-            if (any_first) any_first = __builtin_amdgcn_ballot_w64(!has_prev) != 0;
-#endif
             auto step = [&](auto load) {
                 float ci, cq;
                 interp(ci, cq);
@@ -458,7 +442,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 // (bitwise & keeps each vote one compare pair, no branches)
                 auto reaches = [&](int G) { return (room >= (G - 1) * step_max) & (cap_l >= G); };
                 int kg = 0;
-#if QPSK_MM_VOTE4
                 // the four votes are independent: issue them back to back as SGPR
                 // masks and pick the count with scalar selects (no VALU <-> SALU
                 // round trip per vote on the round's critical path)
@@ -468,16 +451,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const uint64_t m3 = __builtin_amdgcn_ballot_w64(live & !reaches(kguar + 3));
                 kg = m2 == 0 ? (m3 == 0 ? kguar + 3 : kguar + 2)
                              : (m1 == 0 ? kguar + 1 : (m0 == 0 ? kguar : 0));
-#else
-                if (__ballot(live & !reaches(kguar + 2)) == 0) {
-                    kg = kguar + 2;
-                    if (__ballot(live & !reaches(kguar + 3)) == 0) kg = kguar + 3;
-                } else if (__ballot(live & !reaches(kguar + 1)) == 0) {
-                    kg = kguar + 1;
-                } else if (__ballot(live & !reaches(kguar)) == 0) {
-                    kg = kguar;
-                }
-#endif
                 kg = __builtin_amdgcn_readfirstlane(kg);
                 kuni = kg > 0 ? kg : 0;
                 ACC(c_pre, tl);
@@ -509,11 +482,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                     return (base + 2 < rend) & (k < kmax) &
                            (last | (static_cast<double>(rend - d - 3) - nt >= lag_max));
                 };
-#if QPSK_MM_VOTE4
                 if (__builtin_amdgcn_ballot_w64(more()) != 0) {   // one vote skips the loop in steady state
-#else
-                if (__ballot(more()) != 0) {   // one vote skips the loop in steady state
-#endif
                     reload();                   // the uniform loop ended on a tap-less step
                     while (more()) step(std::true_type{});
                 }
