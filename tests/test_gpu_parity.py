@@ -441,3 +441,18 @@ def test_host_ring_errors():
     ring.collect()
     ring.close()
     b.close()
+
+
+def test_c_abi_demo_from_plain_c():
+    """The boundary from plain C, the way a cgo / JNI / P/Invoke binding calls it:
+    tools/c_abi_demo (built by build()) demodulates ragged calls through
+    qpsk_demod_process and the qpsk_rx ring and checks every call's bits against
+    the oracle's DeModulate."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tools", "bin", "c_abi_demo")
+    assert os.path.exists(exe), "run __graft_entry__.build() (make -f tools/c_abi_demo.mk)"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "bits identical to the oracle" in r.stdout
