@@ -27,15 +27,19 @@
 static const double or_sincos_table[1024] = { OR_SINCOS_TAB_VALUES_HI };
 static const double or_sincos_table_lo[1024] = { OR_SINCOS_TAB_VALUES_LO };
 
-/* argument the table reduction accepts: |x| <= 1e6 (or NaN).  Larger |x| and
- * +-Inf are pre-reduced with fmod (Inf -> NaN); the Costas loop, whose theta
- * is wrapped to about [-pi, pi], applies this only after a wrap. */
+/* argument the table reduction accepts: |x| <= 2^40 (or NaN).  Up to there the
+ * Cody-Waite step is exact: k = rint(x*256/pi) < 2^49, x - k*P1 is a multiple
+ * of 2^-59 below 2^-6 (so the first fma is exact), and k*P3 leaves < 2^-120.
+ * Larger |x| and +-Inf are pre-reduced with fmod (Inf -> NaN).  The Costas
+ * loop's theta leaves [-pi, pi] only once its freq passes pi (a QPSK false
+ * lock at a multiple of pi/2 per symbol): theta then grows by ~freq per
+ * symbol, which a sustained run reaches within a few calls. */
 static inline double or_sincos_arg(double x)
 {
-    return fabs(x) > 1.0e6 ? fmod(x, 6.28318530717958647693) : x;
+    return fabs(x) > 0x1p40 ? fmod(x, 6.28318530717958647693) : x;
 }
 
-/* sin and cos of x, |x| <= 1e6 or NaN, given the 512-entry table (any address
+/* sin and cos of x, |x| <= 2^40 or NaN, given the 512-entry table (any address
  * space: the GPU kernels pass a copy staged in LDS).  Straight-line: the GPU
  * Costas loop is issue-bound and every instruction costs issue slots.  NaN
  * propagates (any table index gives NaN). */
@@ -50,7 +54,7 @@ static inline void or_sincos_tab_core(double x, const double *tab, const double 
     const double S3 = -0x1.5555555555555p-3, S5 = 0x1.1111111111111p-7;    /* -1/6, 1/120 */
     const double C4 = 0x1.5555555555555p-5, C6 = -0x1.6c16c16c16c17p-10;  /* 1/24, -1/720 */
     /* kb = x*256/pi + 1.5*2^52 rounds to an integer (ties to even), so
-     * k = kb - 1.5*2^52 = rint(x*256/pi) exactly (|x| <= 1e6) and the low
+     * k = kb - 1.5*2^52 = rint(x*256/pi) exactly (|x| <= 2^40) and the low
      * mantissa bits of kb are k mod 512 in two's complement: the table index
      * without a separate rint */
     union { double d; unsigned long long u; } kb;
@@ -77,7 +81,7 @@ static inline void or_sincos_tab_core(double x, const double *tab, const double 
 static inline void or_sincos_tab(double x, const double *tab, const double *lo, double *s,
                                       double *c)
 {
-    if (__builtin_expect(fabs(x) > 1.0e6, 0)) x = or_sincos_arg(x);
+    if (__builtin_expect(fabs(x) > 0x1p40, 0)) x = or_sincos_arg(x);
     or_sincos_tab_core(x, tab, lo, s, c);
 }
 

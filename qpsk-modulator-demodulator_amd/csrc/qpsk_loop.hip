@@ -605,8 +605,13 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             f2 *out = L.rot + (slot * SPW + lane) * L.RS;
             d2 y;
             // CostasLoopQpsk.cs:63-92: double NCO, float I/O (y widened to double).
-            // HUGE: theta may exceed the table reduction's range (qpsk_sincos_arg);
-            // the fast pass assumes it does not and the round is redone if it did.
+            // HUGE: theta may exceed the table reduction's range (|theta| <= 2^40,
+            // qpsk_sincos_arg); the fast pass assumes it does not and the round is
+            // redone if it did.  Below 2^40 the fast pass is exact: a stream in a
+            // QPSK false lock (|freq| > pi, theta growing every symbol) keeps the
+            // fast path for ~10^5 calls (profiles/r02_state_c3.log: a 4096-stream
+            // C3 batch has 27 such streams after 6 calls; with the old 1e6 range
+            // their 26 workgroups redid every round and the kernel took 2.7x)
             auto widen = [](sym_t v) { return from_sym(v); };
             auto step = [&](int k, auto huge) {
                 const d2 yn = widen(in[k + 1]);   // next symbol, read and widened under this one's chain
@@ -669,7 +674,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 amax = fmax(amax, fabs(theta));
             }
             // fmax drops NaN, which the fast path handles exactly like the full one
-            if (__builtin_expect(__ballot(mine && amax > 1.0e6) != 0, 0)) {
+            if (__builtin_expect(__ballot(mine && amax > 0x1p40) != 0, 0)) {
                 theta = theta0;
                 freq = freq0;
                 y = widen(in[0]);

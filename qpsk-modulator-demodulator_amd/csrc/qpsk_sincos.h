@@ -38,12 +38,16 @@ static __device__ const double qpsk_sincos_table_dev[1024] = { QPSK_SINCOS_TAB_V
 static __device__ const double qpsk_sincos_table_dev_lo[1024] = { QPSK_SINCOS_TAB_VALUES_LO };
 #endif
 
-/* argument the table reduction accepts: |x| <= 1e6 (or NaN).  Larger |x| and
- * +-Inf are pre-reduced with fmod (Inf -> NaN); the Costas loop, whose theta
- * is wrapped to about [-pi, pi], applies this only after a wrap. */
+/* argument the table reduction accepts: |x| <= 2^40 (or NaN).  Up to there the
+ * Cody-Waite step is exact: k = rint(x*256/pi) < 2^49, x - k*P1 is a multiple
+ * of 2^-59 below 2^-6 (so the first fma is exact), and k*P3 leaves < 2^-120.
+ * Larger |x| and +-Inf are pre-reduced with fmod (Inf -> NaN).  The Costas
+ * loop's theta leaves [-pi, pi] only once its freq passes pi (a QPSK false
+ * lock at a multiple of pi/2 per symbol): theta then grows by ~freq per
+ * symbol, which a sustained run reaches within a few calls. */
 QPSK_HD static inline double qpsk_sincos_arg(double x)
 {
-    return fabs(x) > 1.0e6 ? fmod(x, 6.28318530717958647693) : x;
+    return fabs(x) > 0x1p40 ? fmod(x, 6.28318530717958647693) : x;
 }
 
 /* the core's constants; a caller may hold them in registers (device loops pin
@@ -66,7 +70,7 @@ QPSK_HD static inline void qpsk_sincos_tab_core_k(double x, const double *tab, c
                                              const qpsk_sincos_consts *K, double *s, double *c)
 {
     /* kb = x*256/pi + 1.5*2^52 rounds to an integer (ties to even), so
-     * k = kb - 1.5*2^52 = rint(x*256/pi) exactly (|x| <= 1e6) and the low
+     * k = kb - 1.5*2^52 = rint(x*256/pi) exactly (|x| <= 2^40) and the low
      * mantissa bits of kb are k mod 512 in two's complement: the table index
      * without a separate rint */
     union { double d; unsigned long long u; } kb;
@@ -114,7 +118,7 @@ QPSK_HD static inline void qpsk_sincos_tab_core_f(double x, const double *tab, c
     *c = tc + fma(-ts, r, fma(-ts, r3p, fma(tc, cm, lc)));
 }
 
-/* sin and cos of x, |x| <= 1e6 or NaN, given the 512-entry table (any address
+/* sin and cos of x, |x| <= 2^40 or NaN, given the 512-entry table (any address
  * space: the GPU kernels pass a copy staged in LDS).  Straight-line: the GPU
  * Costas loop is issue-bound and every instruction costs issue slots.  NaN
  * propagates (any table index gives NaN). */
@@ -129,7 +133,7 @@ QPSK_HD static inline void qpsk_sincos_tab_core(double x, const double *tab, con
 QPSK_HD static inline void qpsk_sincos_tab(double x, const double *tab, const double *lo, double *s,
                                       double *c)
 {
-    if (__builtin_expect(fabs(x) > 1.0e6, 0)) x = qpsk_sincos_arg(x);
+    if (__builtin_expect(fabs(x) > 0x1p40, 0)) x = qpsk_sincos_arg(x);
     qpsk_sincos_tab_core(x, tab, lo, s, c);
 }
 

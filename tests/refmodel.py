@@ -186,7 +186,7 @@ SINCOS_TABLE = _table()
 
 
 def portable_sincos(x):
-    if not (abs(x) <= 1.0e6):   # huge, +-Inf (-> NaN) and NaN
+    if not (abs(x) <= 2.0 ** 40):   # huge, +-Inf (-> NaN) and NaN
         if math.isnan(x) or math.isinf(x):
             return math.nan, math.nan
         x = math.fmod(x, 6.28318530717958647693)
