@@ -4,24 +4,40 @@
 Metric (BASELINE.json): complex MSa/s through the full demod chain (batched
 streams), whole job over all ranks, inputs resident in HBM.
 
-  python bench.py --gpus N --steps K --warmup W [--config c2|c3|c5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5]
 
 One step = one DeModulate call (QPSKDeModulator.cs:345-425) on every stream of
 the rank's batch: matched-filter FIR -> Mueller-Muller + Costas + differential
-decode -> packed bits, all on the GPU.  Streams are independent
-(QPSKDeModulator.cs:20-73), so ranks shard streams with no data-path
-collective ("scaling": "weak": each rank owns its own 256-stream C2 batch);
-the only collectives are the MAX of the timed region and the sums of the
-parity / BER counters after it.
+decode -> packed bits, all on the GPU.
 
-Rank 0 at N=1 also times the CPU oracle (the C restatement of the reference's
-SIMD C# path, `"kind": "port"`) on the same generated buffer.
+Headline workload (`value`): C3, the largest single-GPU configuration of
+BASELINE.json (4096 streams x 2^20 complex samples per GPU, sps 4, 129-tap
+RRC).  Streams are independent (QPSKDeModulator.cs:20-73), so ranks shard
+streams with no data-path collective ("scaling": "weak": every rank owns its
+own C3-shaped batch); the only collectives are the MAX of the timed region and
+the sums of the parity / BER counters after it.  The other configs run after
+the headline as `sub_records` (N=1: C2 and C5; N>1: the C4 shard shape, 4096
+streams/GPU at sps 8, plus the RCCL scatter/gather leg of SURVEY.md 8e).
+
+After each config's timed region (never inside it) the timed handle itself is
+checked: one call from the initial state on every stream, whose bit rows are
+compared with the CPU oracle run on the host cores (glibc trig, what .NET on
+Linux calls) -- the same run is the `cpu_baseline` -- over as many streams as
+fit the CPU time budget, always including the last 64 rows of the batch
+(row offsets past 4 GiB at C3/C5).  Rank 0 at N=1 only; at N>1 every rank
+checks the first and last two streams of its shard against the portable-trig
+oracle.
+
+--gpus N without a launcher spawns `torch.distributed.run` with N ranks
+before anything touches the GPU, and exits with its status.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,6 +50,7 @@ for _p in (PKG, os.path.join(ROOT, "oracle")):
 FS = 10_000_000
 ALPHA = 0.4000000059604645            # (double)0.4f, testAtDataLevel.cs:18
 HBM_PEAK_GBS = 8000.0                 # MI355X_MICROARCH.md chip table (spec)
+FP32_PEAK_TFLOPS = 157.3              # MI355X_MICROARCH.md: peak FP32 vector (spec)
 METRIC = "complex MSa/s through full demod chain (batched streams); BER vs CPU ref"
 
 CONFIGS = {
@@ -41,7 +58,7 @@ CONFIGS = {
     "c2": dict(streams=256, sps=8, span=8, impaired=False, fll=False,
                name="C2: 256 streams x 2^20 complex samples, sps=8, 65-tap RRC, clean +-1ppm LOs"),
     "c3": dict(streams=4096, sps=4, span=32, impaired=False, fll=False,
-               name="C3: 4096 streams x 2^20 complex samples, sps=4, 129-tap RRC"),
+               name="C3: 4096 streams x 2^20 complex samples, sps=4, 129-tap RRC, clean +-1ppm LOs"),
     "c4": dict(streams=4096, sps=8, span=8, impaired=False, fll=False,
                name="C4 shard: 4096 streams/GPU x 2^20 complex samples, sps=8, 65-tap RRC"),
     "c5": dict(streams=8192, sps=8, span=8, impaired=True, fll=True,
@@ -90,34 +107,157 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(host_iq, sps, span, n_threads, fll=False):
+def cpu_quota():
+    """CPUs this process may use per cgroup v2 cpu.max (None = unlimited)."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+# ---------------------------------------------------------------------------
+# parity of the timed handle against the CPU oracle
+# ---------------------------------------------------------------------------
+def compare_rows(gpu_bits, gpu_nb, ref_bits, ref_nb, gpu_syms=None, gpu_ns=None, ref_syms=None,
+                 ref_ns=None):
+    """Per-stream comparison of packed bit rows (+ symbols when both sides
+    have them).  Returns (mismatching stream indices, max |symbol error|)."""
     import numpy as np
+    bad = []
+    max_err = 0.0
+    for i in range(len(ref_nb)):
+        nb = int(ref_nb[i])
+        ok = int(gpu_nb[i]) == nb
+        if ok and nb:
+            full = nb // 8
+            ok = np.array_equal(gpu_bits[i, :full], ref_bits[i, :full])
+            if ok and nb % 8:
+                m = (0xFF << (8 - nb % 8)) & 0xFF
+                ok = (int(gpu_bits[i, full]) & m) == (int(ref_bits[i, full]) & m)
+        if ok and gpu_syms is not None and ref_syms is not None:
+            ns = int(ref_ns[i])
+            ok = int(gpu_ns[i]) == ns
+            if ok and ns:
+                d = np.abs(gpu_syms[i, : 2 * ns].astype(np.float64) - ref_syms[i, : 2 * ns])
+                max_err = max(max_err, float(np.nanmax(d)) if d.size else 0.0)
+        if not ok:
+            bad.append(i)
+    return bad, max_err
+
+
+def rows_to_host(t, idx):
+    """Rows idx of a device tensor as one host numpy array, copied range by
+    range (no device-side gather: the C5 batch leaves no HBM for one)."""
+    import numpy as np
+    parts = []
+    a = 0
+    while a < len(idx):
+        b = a
+        while b + 1 < len(idx) and idx[b + 1] == idx[b] + 1:
+            b += 1
+        parts.append(t[idx[a]: idx[b] + 1].cpu().numpy())
+        a = b + 1
+    return parts[0] if len(parts) == 1 else np.concatenate(parts)
+
+
+def pick_streams(S, n_cover, tail=64):
+    """Stream indices the CPU leg covers: all of them when the budget allows,
+    else the first n_cover - tail and the last `tail` (the rows furthest into
+    the batch buffers)."""
+    if n_cover >= S:
+        return list(range(S))
+    head = max(1, n_cover - tail)
+    return list(range(head)) + list(range(S - tail, S))
+
+
+def cpu_leg(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, n, budget_s, threads, single_streams=8):
+    """CPU baseline + parity at scale: the oracle (glibc trig) on the host
+    cores over a time-bounded subset of the timed batch, timed, and its bit
+    rows / symbols compared with the GPU's rows of the same streams."""
+    import numpy as np
+    import torch
     import oracle as O
+    S = iq.shape[0]
+    sps, span = cfg["sps"], cfg["span"]
+    kw = dict(rrc_alpha=ALPHA, rrc_span=span, trig=O.TRIG_LIBM, enable_fll=cfg["fll"])
+    # single core on the first streams: the per-stream cost that sizes the rest
+    ns1 = min(S, single_streams)
+    host1 = iq[:ns1].cpu().numpy()
     t0 = time.perf_counter()
-    nb = O.demod_batch_timed(host_iq, FS, FS // sps, n_threads=n_threads, rrc_alpha=ALPHA,
-                             rrc_span=span, trig=O.TRIG_LIBM, enable_fll=fll)
+    O.demod_batch_packed(host1, FS, FS // sps, n_threads=1, want_bits=False, **kw)
+    dt1 = time.perf_counter() - t0
+    per_stream = dt1 / ns1
+    eff = min(threads, cpu_quota() or threads)
+    n_cover = max(min(S, 64 + 8), int(budget_s * eff / per_stream))
+    idx = pick_streams(S, n_cover)
+    host = rows_to_host(iq, idx)
+    want_syms = syms_dev is not None
+    t0 = time.perf_counter()
+    rb, rnb, rsy, rns = O.demod_batch_packed(host, FS, FS // sps, n_threads=threads,
+                                             want_syms=want_syms, **kw)
     dt = time.perf_counter() - t0
-    S, nf = host_iq.shape
-    return S * (nf // 2) / dt / 1e6, dt, int(np.sum(nb))
+    del host
+    gb = rows_to_host(bits_dev, idx)
+    gnb = rows_to_host(nbits_dev, idx)
+    gsy = rows_to_host(syms_dev, idx) if want_syms else None
+    gns = rows_to_host(nsyms_dev, idx) if want_syms else None
+    bad, max_err = compare_rows(gb, gnb, rb, rnb, gsy, gns, rsy, rns)
+    rate = len(idx) * n / dt / 1e6
+    cpu = {"value": round(rate, 2), "unit": "MSa/s", "cores": threads, "kind": "port",
+           "single_core": round(ns1 * n / dt1 / 1e6, 2), "cpu_model": cpu_model(),
+           "host_cpus": os.cpu_count(), "cpu_quota_cpus": cpu_quota(),
+           "sample": (f"{len(idx)} of {S} streams x {n} samples "
+                      + ("(the whole batch)" if len(idx) == S else
+                         f"(first {len(idx) - 64} + last 64)")
+                      + f", one oracle demodulator per stream (glibc trig"
+                      + (", FLL on" if cfg["fll"] else "") + f") on {threads} host threads, "
+                      f"{dt:.2f} s wall; single_core: first {ns1} streams on 1 thread, {dt1:.2f} s")}
+    if cpu["cpu_quota_cpus"] and cpu["cpu_quota_cpus"] < threads:
+        cpu["note"] = (f"the box's cgroup grants {cpu['cpu_quota_cpus']:g} CPUs of quota, so "
+                       f"{threads} threads run at that rate; single_core x 128 physical cores "
+                       f"= {round(cpu['single_core'] * 128, 1)} MSa/s is the unthrottled all-core "
+                       "estimate (an extrapolation, not a measurement)")
+    parity = {"oracle": "CPU oracle, glibc trig (what .NET on Linux calls)",
+              "streams": len(idx), "first_stream": idx[0], "last_stream": idx[-1],
+              "mismatching_streams": len(bad), "mismatch_examples": bad[:8],
+              "max_sym_err": (round(max_err, 9) if want_syms else None),
+              "sym_tol": 1e-5 if not cfg["fll"] else 1e-4,
+              "max_row_offset_GiB": round(idx[-1] * iq.stride(0) * 4 / 2**30, 2)}
+    if not want_syms:
+        parity["note"] = "bits only: no HBM left for a symbol copy of the whole batch"
+    return cpu, parity
 
 
-def parity_check(iq_dev, cfg, n, n_check=2):
-    """Fresh 2-stream batch vs the oracle on the same samples: bits and symbols."""
+def portable_check(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, idx):
+    """Bit-exact check (bits AND symbols) of a few streams of the timed handle
+    against the portable-trig oracle, which shares the GPU's sincos."""
     import numpy as np
+    import torch
     import oracle as O
-    import qpsk_amd as Q
-    host = iq_dev[:n_check].cpu().numpy()
-    b = Q.BatchDemodulator(n_check, Q.params(FS, FS // cfg["sps"], ALPHA, cfg["span"],
-                                             enable_fll=cfg["fll"], max_samples_per_call=n))
-    bits, nb, syms, ns = b.process(host, want_syms=True)
-    b.close()
-    ok = True
-    for s in range(n_check):
-        dm = O.OracleDemod(FS, FS // cfg["sps"], ALPHA, cfg["span"], enable_fll=cfg["fll"])
-        ob, osy, _ = dm.demodulate_ex(host[s])
-        ok &= Q.unpack_bits(bits[s], int(nb[s])) == ob
-        ok &= bool(np.array_equal(syms[s, : 2 * int(ns[s])], osy))
-    return ok
+    host = rows_to_host(iq, idx)
+    rb, rnb, rsy, rns = O.demod_batch_packed(host, FS, FS // cfg["sps"], n_threads=len(idx),
+                                             want_syms=syms_dev is not None, rrc_alpha=ALPHA,
+                                             rrc_span=cfg["span"], trig=O.TRIG_PORTABLE,
+                                             enable_fll=cfg["fll"])
+    gb = rows_to_host(bits_dev, idx)
+    gnb = rows_to_host(nbits_dev, idx)
+    bad, err = compare_rows(gb, gnb, rb, rnb)
+    sym_bad = 0
+    if syms_dev is not None:
+        gsy = rows_to_host(syms_dev, idx)
+        gns = rows_to_host(nsyms_dev, idx)
+        for i in range(len(idx)):
+            ns = int(rns[i])
+            if int(gns[i]) != ns or not np.array_equal(gsy[i, : 2 * ns], rsy[i, : 2 * ns]):
+                sym_bad += 1
+    return len(bad), sym_bad
 
 
 def ber_after_lock(bits_dev, nbits_dev, tx_dev, n_streams, skip_bits=8000, window=2048,
@@ -132,9 +272,9 @@ def ber_after_lock(bits_dev, nbits_dev, tx_dev, n_streams, skip_bits=8000, windo
     or an error in it) or whose offset changes inside them (last `key_bits`
     misaligned) are reported as `lost_windows`, not as bit errors."""
     import numpy as np
-    nb = nbits_dev.cpu().numpy()
-    bits = bits_dev.cpu().numpy()
-    tx = tx_dev.cpu().numpy()
+    nb = nbits_dev[:n_streams].cpu().numpy()
+    bits = bits_dev[:n_streams].cpu().numpy()
+    tx = tx_dev[:n_streams].cpu().numpy()
     errs = total = lost = slips = 0
     for s in range(n_streams):
         rx = np.unpackbits(bits[s])[: int(nb[s])]
@@ -169,61 +309,59 @@ def ber_after_lock(bits_dev, nbits_dev, tx_dev, n_streams, skip_bits=8000, windo
     return errs, total, lost, slips
 
 
-def split_gather(demod, fresh_state, iq_local, bits, nbits, S, n, world, rank, dev, synth_kw,
-                 backend):
-    """The RCCL leg of SURVEY.md §8e, measured after the no-collective bench:
-    rank 0 synthesises the whole batch and scatters the stream shards over
-    xGMI, every rank demodulates its shard, and rank 0 gathers the packed
-    bits and bit counts.  Returns per-phase times (max over ranks) and whether
-    every scattered shard equals the one the rank generated itself."""
+# ---------------------------------------------------------------------------
+# the RCCL leg of SURVEY.md §8e
+# ---------------------------------------------------------------------------
+def split_gather(synth, demod_shard, S, n, world, rank, dev, host_collectives):
+    """Rank 0 synthesises the whole batch and scatters the stream shards,
+    every rank demodulates its shard, and rank 0 gathers the packed bit rows
+    and bit counts.  `synth(first_stream, count)` returns [count, 2n] float32
+    rows (stream ids are global, so a shard is the same whatever the world
+    size); `demod_shard(x)` returns (bits [S, B] uint8, n_bits [S] int64).
+    Returns per-phase times (max over ranks), the gathered rows on rank 0, and
+    whether every scattered shard equals the one the rank synthesised itself.
+    host_collectives: gloo (CPU tensors) instead of RCCL (device tensors)."""
     import torch
     import torch.distributed as dist
-    import qpsk_amd as Q
-    total_bytes = world * S * 2 * n * 4
-    if total_bytes > (48 << 30):
-        return {"skipped": f"whole batch {total_bytes / 2**30:.0f} GiB does not fit one GPU; "
-                           "each rank synthesises its own shard (no split)"}
-    host = backend != "nccl"          # gloo rehearsal: collectives on host tensors
-    full = None
-    if rank == 0:
-        full, _ = Q.synth_generate(world * S, n, FS, synth_kw["rs"], rrc_alpha=ALPHA,
-                                   rrc_span=synth_kw["span"], seed=0x5159534B, first_stream=0,
-                                   lo_ppm=1.0, cfo_hz=synth_kw["cfo"], multipath=synth_kw["mp"],
-                                   esn0_db=synth_kw["esn0"], device=dev.index)
-        if host:
-            full = full.cpu()
-    shard = torch.empty((S, 2 * n), dtype=torch.float32, device="cpu" if host else dev)
+    cdev = torch.device("cpu") if host_collectives else dev
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    full = synth(0, world * S).to(cdev) if rank == 0 else None
     chunks = list(full.chunk(world, dim=0)) if rank == 0 else None
-    torch.cuda.synchronize(dev)
+    shard = torch.empty((S, 2 * n), dtype=torch.float32, device=cdev)
+    sync()
     dist.barrier()
     t0 = time.perf_counter()
     dist.scatter(shard, chunks, src=0)
-    torch.cuda.synchronize(dev)
+    sync()
     t1 = time.perf_counter()
-    x = shard.to(dev) if host else shard
-    demod.set_state(fresh_state)
-    demod.process_device(x, n, bits, nbits)
-    torch.cuda.synchronize(dev)
+    bits, nbits = demod_shard(shard.to(dev))
+    sync()
     t2 = time.perf_counter()
-    b, c = (bits.cpu(), nbits.cpu()) if host else (bits, nbits)
+    b, c = bits.to(cdev), nbits.to(cdev)
     gb = [torch.empty_like(b) for _ in range(world)] if rank == 0 else None
     gc = [torch.empty_like(c) for _ in range(world)] if rank == 0 else None
     dist.gather(b, gb, dst=0)
     dist.gather(c, gc, dst=0)
-    torch.cuda.synchronize(dev)
+    sync()
     t3 = time.perf_counter()
-    same = int(torch.equal(x, iq_local))
+    lo, _ = shard_streams(world * S, rank, world)
+    same = int(torch.equal(shard, synth(lo, S).to(cdev)))
     del full, chunks
-    tt = torch.tensor([t1 - t0, t2 - t1, t3 - t2], dtype=torch.float64,
-                      device="cpu" if host else dev)
-    ok = torch.tensor([same], dtype=torch.int64, device="cpu" if host else dev)
+    tt = torch.tensor([t1 - t0, t2 - t1, t3 - t2], dtype=torch.float64, device=cdev)
+    ok = torch.tensor([same], dtype=torch.int64, device=cdev)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     ts, td, tg = (float(v) for v in tt.tolist())
-    return {"scatter_ms": round(ts * 1e3, 3), "demod_ms": round(td * 1e3, 3),
-            "gather_ms": round(tg * 1e3, 3),
-            "value_with_split_gather": round(world * S * n / (ts + td + tg) / 1e6, 2),
-            "shards_match_local_synth": bool(ok.item())}
+    rec = {"scatter_ms": round(ts * 1e3, 3), "demod_ms": round(td * 1e3, 3),
+           "gather_ms": round(tg * 1e3, 3),
+           "value_with_split_gather": round(world * S * n / (ts + td + tg) / 1e6, 2),
+           "shards_match_local_synth": bool(ok.item())}
+    gathered = (torch.cat(gb).cpu(), torch.cat(gc).cpu()) if rank == 0 else None
+    return rec, gathered
 
 
 TSC_BITS = "11001010011101100100100110101100" + "01110100111001011010001101101001"  # testAtDataLevel.cs:20-22
@@ -302,73 +440,70 @@ def framer_pass(bits, nbits, S, stream, reps=5):
             "bits_GBps": round(row_bytes / (t_push / reps * 1e-3) / 1e9, 1) if t_push > 0 else None}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--samples", type=int, default=1 << 20)
-    ap.add_argument("--loop-variant", type=int, default=0,
-                    help="symbol-loop kernel shape (qpsk_demod_params.loop_variant; 0 = auto)")
-    ap.add_argument("--streams", type=int, default=0, help="override streams per GPU")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="gloo + --share-gpu rehearses the N>1 path on a one-GPU box")
-    ap.add_argument("--timed-only", action="store_true",
-                    help="warmup + timed steps only (no BER, parity, framer, split/gather, host ring, "
-                         "CPU baseline): the command rocprofv3 traces, so its kernel averages are "
-                         "the timed region's")
-    ap.add_argument("--no-host-ring", action="store_true",
-                    help="skip the PCIe-inclusive host-ring pass (run at N=1 for batches <= 4 GiB)")
-    ap.add_argument("--no-framer", action="store_true",
-                    help="skip the device TSC + framer pass measured beside the headline")
-    ap.add_argument("--no-split-gather", action="store_true",
-                    help="skip the RCCL scatter/demod/gather pass that runs when N > 1")
-    ap.add_argument("--serial-calls", action="store_true",
-                    help="synchronous process() per step (no front/back stage overlap)")
-    ap.add_argument("--share-gpu", action="store_true",
-                    help="every rank uses cuda:0 (rehearsal only; numbers meaningless)")
-    args = ap.parse_args()
-    if args.timed_only:
-        args.no_parity = args.no_framer = args.no_split_gather = True
-        args.no_host_ring = args.no_cpu_baseline = True
+def rooflines(st, S, n, cfg):
+    """Per-kernel rooflines from the stage events of the timed region
+    (algorithmic bytes / flops per unit)."""
+    sps, T = cfg["sps"], cfg["span"] * cfg["sps"] + 1
+    out = {}
+    if st["fir"] > 0:
+        fir_s = st["fir"] / 1e3
+        gbs = 16.0 * S * n / fir_s / 1e9             # 8 B in + 8 B out per complex sample
+        tfl = 4.0 * T * S * n / fir_s / 1e12         # real taps x complex data: 2 mul + 2 add per tap
+        out["fir"] = {"kernel": "fir_tile_kernel (RRC matched filter)", "ms": round(st["fir"], 4),
+                      "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(gbs / HBM_PEAK_GBS, 4),
+                      "valu_tflops": round(tfl, 2), "valu_peak_tflops": FP32_PEAK_TFLOPS,
+                      "valu_frac": round(tfl / FP32_PEAK_TFLOPS, 4),
+                      "per_unit": f"16 B and {4 * T} flop per complex sample, {S * n} samples per launch"}
+    if st["loop"] > 0:
+        loop_s = st["loop"] / 1e3
+        b = (8.0 + 0.25 / sps) * S * n               # MF samples in + packed bits out
+        syms = S * n / sps
+        out["loop"] = {"kernel": "loop_kernel (M&M + Costas + decode)", "ms": round(st["loop"], 4),
+                       "bound": "latency (serial per-stream recurrence)",
+                       "achieved": round(b / loop_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(b / loop_s / 1e9 / HBM_PEAK_GBS, 4),
+                       "ns_per_symbol_per_stream": round(loop_s / (n / sps) * 1e9, 2),
+                       "per_unit": f"{8 + 0.25 / sps:.4f} B per complex sample, {S * n} samples, "
+                                   f"{int(syms)} symbols per launch"}
+    if st["fll"] > 0.01:
+        fll_s = st["fll"] / 1e3
+        tfl = 640.0 * S * n / fll_s / 1e12
+        out["fll"] = {"kernel": "fll_sys_kernel (Band-Edge FLL)", "ms": round(st["fll"], 4),
+                      "bound": "latency/VALU (serial per-stream feedback)",
+                      "achieved": round(16.0 * S * n / fll_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(16.0 * S * n / fll_s / 1e9 / HBM_PEAK_GBS, 4),
+                      "valu_tflops": round(tfl, 2), "valu_frac": round(tfl / FP32_PEAK_TFLOPS, 4),
+                      "per_unit": "16 B and 640 flop (+ one sincos) per complex sample"}
+    return out
 
+
+# ---------------------------------------------------------------------------
+# one configuration
+# ---------------------------------------------------------------------------
+def run_config(key, args, rank, world, dev, steps, warmup, headline):
     import torch
     import torch.distributed as dist
     import qpsk_amd as Q
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", 0))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
-
-    cfg = dict(CONFIGS[args.config])
+    cfg = dict(CONFIGS[key])
     S = args.streams or cfg["streams"]
     n = args.samples
     sps, span = cfg["sps"], cfg["span"]
     rs = FS // sps
+    nccl = args.dist_backend == "nccl"
     # weak scaling: the job is world*S streams, rank r owns the contiguous
     # shard [lo, hi); every stream's payload/LO/noise seeds follow its global id
     lo, hi = shard_streams(world * S, rank, world)
     assert hi - lo == S
-    iq, tx = Q.synth_generate(S, n, FS, rs, rrc_alpha=ALPHA, rrc_span=span,
-                              seed=0x5159534B, first_stream=lo, lo_ppm=1.0,
-                              cfo_hz=5000.0 if cfg["impaired"] else 0.0,
-                              multipath=cfg["impaired"], esn0_db=20.0 if cfg["impaired"] else None,
-                              device=local)
-    p = Q.params(FS, rs, ALPHA, span, enable_fll=cfg["fll"], device=local, max_samples_per_call=n,
+    synth_kw = dict(rrc_alpha=ALPHA, rrc_span=span, seed=0x5159534B, lo_ppm=1.0,
+                    cfo_hz=5000.0 if cfg["impaired"] else 0.0, multipath=cfg["impaired"],
+                    esn0_db=20.0 if cfg["impaired"] else None, device=dev.index)
+    iq, tx = Q.synth_generate(S, n, FS, rs, first_stream=lo, **synth_kw)
+    p = Q.params(FS, rs, ALPHA, span, enable_fll=cfg["fll"], device=dev.index, max_samples_per_call=n,
                  loop_variant=args.loop_variant)
     demod = Q.BatchDemodulator(S, p)
-    fresh_state = demod.get_state()   # for the BER pass (no second handle: C5 needs ~192 GiB)
+    fresh_state = demod.get_state()   # for the parity / BER call (no second handle: C5 needs ~256 GiB)
     # a real stream (torch's legacy default is handle 0, which the C ABI reads
     # as "library-owned"); torch ops and the demod then share one order
     stream = torch.cuda.Stream(dev)
@@ -391,7 +526,7 @@ def main():
         if not args.serial_calls:
             demod.pipeline_wait()
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     drain()
     torch.cuda.synchronize(dev)
@@ -400,7 +535,7 @@ def main():
     torch.cuda.synchronize(dev)
     demod.enable_timing(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     drain()
     torch.cuda.synchronize(dev)
@@ -411,64 +546,54 @@ def main():
     st = demod.stage_times()
     demod.enable_timing(False)
 
-    # untimed: BER of one call from the initial state (stream starts at t=0)
+    rec = {}
     errs = total_bits = lost = slips = 0
+    bad_bits = bad_syms = n_port = 0
     if not args.timed_only:
+        # untimed: one call from the initial state on every stream of the timed
+        # handle (stream starts at t=0); its rows feed parity and BER
+        syms = nsyms = None
+        if not cfg["fll"]:   # the FLL batches leave no HBM for a symbol copy
+            try:
+                syms = torch.empty((S, 2 * ms), dtype=torch.float32, device=dev)
+                nsyms = torch.zeros(S, dtype=torch.int64, device=dev)
+            except torch.OutOfMemoryError:
+                syms = nsyms = None
         demod.set_state(fresh_state)
-        demod.process_device(iq, n, bits, nbits)
+        demod.process_device(iq, n, bits, nbits, syms_dev=syms, n_syms_dev=nsyms)
         torch.cuda.synchronize(dev)
         errs, total_bits, lost, slips = ber_after_lock(bits, nbits, tx, min(S, 32))
-    parity_ok = True
-    if rank == 0 and not args.no_parity:
-        parity_ok = parity_check(iq, cfg, n)
-    t_max, (errs, total_bits, lost, slips, bad) = reduce_stats(
-        elapsed, [errs, total_bits, lost, slips, 0 if parity_ok else 1],
-        device=dev if args.dist_backend == "nccl" else None)
+        if not args.no_parity:
+            idx = [0, 1, S - 2, S - 1] if S >= 4 else list(range(S))
+            bad_bits, bad_syms = portable_check(iq, bits, nbits, syms, nsyms, cfg, idx)
+            n_port = len(idx)
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                threads = args.cpu_threads or (os.cpu_count() or 1)
+                rec["cpu_baseline"], rec["parity_vs_libm_oracle"] = cpu_leg(
+                    iq, bits, nbits, syms, nsyms, cfg, n, args.cpu_seconds, threads)
+        del syms, nsyms
+    t_max, (errs, total_bits, lost, slips, bad_bits, bad_syms, n_port) = reduce_stats(
+        elapsed, [errs, total_bits, lost, slips, bad_bits, bad_syms, n_port],
+        device=dev if nccl else None)
 
-    fr_stats = framer_pass(bits, nbits, S, stream) if not args.no_framer else None
-
-    sg = None
-    if world > 1 and not args.no_split_gather:
-        sg = split_gather(demod, fresh_state, iq, bits, nbits, S, n, world, rank, dev,
-                          dict(rs=rs, span=span, cfo=5000.0 if cfg["impaired"] else 0.0,
-                               mp=cfg["impaired"], esn0=20.0 if cfg["impaired"] else None),
-                          args.dist_backend)
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # bounded sample: at most 512 streams (~10 s of CPU work at 2^20 samples)
-        ns = min(S, 512)
-        host = iq[:ns].cpu().numpy()
-        ncpu = os.cpu_count() or 1
-        threads = args.cpu_threads or max(1, min(16, ncpu))
-        v, dt, _ = cpu_baseline(host, sps, span, threads, fll=cfg["fll"])
-        # one core on the first 8 streams (single-core and all-core)
-        v1, dt1, _ = cpu_baseline(host[: min(ns, 8)], sps, span, 1, fll=cfg["fll"])
-        what = f"full {args.config} batch" if ns == S else f"first {ns} of {S} {args.config} streams"
-        cpu = {"value": round(v, 2), "unit": "MSa/s", "cores": threads, "kind": "port",
-               "single_core": round(v1, 2), "cpu_model": cpu_model(), "host_cpus": ncpu,
-               "sample": f"{what} ({ns} streams x {n} samples) on {threads} host threads, "
-                         f"one oracle demodulator (glibc trig{', FLL on' if cfg['fll'] else ''}) per stream, "
-                         f"{dt:.2f} s wall; single_core: first {min(ns, 8)} streams on 1 thread, "
-                         f"{dt1:.2f} s wall"}
-
-    samples_total = world * S * n * args.steps
-    value = samples_total / t_max / 1e6
-    fir_bytes = 16.0 * S * n                      # 8 B in + 8 B out per complex sample
-    fir_s = st["fir"] / 1e3
-    achieved = fir_bytes / fir_s / 1e9 if fir_s > 0 else 0.0
-    # the PMC passes were taken at the config's own shard size; any other
-    # size has no measured traffic
-    traffic = load_traffic(args.config) if (S == cfg["streams"] and n == 1 << 20) else None
-    loop_bytes = (8.0 + 0.25 / sps) * S * n       # MF samples in + packed bits out
-    out = {
+    value = world * S * n * steps / t_max / 1e6
+    rl = rooflines(st, S, n, cfg)
+    dom = max(rl, key=lambda k: rl[k]["ms"]) if rl else None
+    roof = None
+    if dom:
+        r = rl[dom]
+        roof = {"bound": r["bound"], "kernel": r["kernel"], "achieved": r["achieved"], "peak": r["peak"],
+                "unit": r["unit"], "frac": r["frac"], "valu_frac": r.get("valu_frac"),
+                "traffic": (load_traffic(key) if dom == "fir" and S == cfg["streams"] and n == 1 << 20
+                            else None)}
+    rec = {
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "MSa/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(t_max / args.steps * 1e3, 4),
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(t_max / steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -480,30 +605,158 @@ def main():
                    "parallelism": f"stream-shard x{world}",
                    "calls": "serial" if args.serial_calls else
                             f"pipelined (front/back stage overlap, depth {demod.pipeline_depth()})"},
-        "roofline": {"bound": "hbm", "kernel": "fir_tile_kernel (RRC matched filter)",
-                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic},
+        "roofline": roof,
+        "rooflines": rl,
         "stages_ms": {k: round(v, 4) for k, v in st.items()},
-        "loop_kernel": {"bound": "latency (serial per-stream recurrence)",
-                        "achieved_GBps": round(loop_bytes / (st["loop"] / 1e3) / 1e9, 1) if st["loop"] else None},
         "ber_after_lock": {"bit_errors": errs, "bits": total_bits,
                            "ber": (errs / total_bits) if total_bits else None,
                            "lost_windows": lost, "symbol_slips": slips,
                            "streams": min(S, 32) * world},
-        "parity_vs_oracle": ("not checked" if args.no_parity else
-                             "bit-exact" if bad == 0 else "MISMATCH"),
-        "cpu_baseline": cpu,
+        "parity_vs_portable_oracle": (
+            "not checked" if (args.no_parity or args.timed_only) else
+            {"streams": n_port, "bit_mismatch_streams": bad_bits, "symbol_mismatch_streams": bad_syms,
+             "note": "first and last two streams of every rank's shard; bits and symbols must be "
+                     "bit-identical (the oracle shares the GPU's sincos)"}),
+        **rec,
     }
-    if fr_stats is not None:
-        out["framer"] = fr_stats
-    if sg is not None:
-        out["split_gather"] = sg
-    if world == 1 and not args.no_host_ring and S * n * 8 <= (4 << 30):
-        out["host_ring"] = host_ring_pass(demod, iq, S, n)
+    if rec.get("cpu_baseline") is None:
+        rec["cpu_baseline"] = None
+    if headline and world == 1 and not args.no_framer and not args.timed_only:
+        rec["framer"] = framer_pass(bits, nbits, S, stream)
+    if world == 1 and not args.no_host_ring and not args.timed_only and S * n * 8 <= (4 << 30):
+        rec["host_ring"] = host_ring_pass(demod, iq, S, n)
+    demod.close()
+    del demod, iq, tx, bits, nbits
+    torch.cuda.set_stream(torch.cuda.default_stream(dev))
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    return rec
+
+
+def split_gather_leg(args, rank, world, dev, S=256):
+    """§8e scatter / demod / gather on the C2 shard shape (256 streams/rank)."""
+    import torch
+    import qpsk_amd as Q
+    cfg = CONFIGS["c2"]
+    n = args.samples
+    rs = FS // cfg["sps"]
+    if world * S * 2 * n * 4 > (48 << 30):
+        return {"skipped": "whole batch does not fit one GPU"}
+    p = Q.params(FS, rs, ALPHA, cfg["span"], device=dev.index, max_samples_per_call=n)
+    demod = Q.BatchDemodulator(S, p)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    demod.set_stream(stream.cuda_stream)
+    ms = demod.max_symbols(n)
+    bits = torch.zeros((S, (2 * ms + 7) // 8 + 64), dtype=torch.uint8, device=dev)
+    nbits = torch.zeros(S, dtype=torch.int64, device=dev)
+
+    def synth(first, count):
+        x, _ = Q.synth_generate(count, n, FS, rs, rrc_alpha=ALPHA, rrc_span=cfg["span"],
+                                seed=0x5159534B, first_stream=first, lo_ppm=1.0, device=dev.index)
+        return x
+
+    def demod_shard(x):
+        demod.process_device(x, n, bits, nbits)
+        return bits, nbits
+
+    rec, _ = split_gather(synth, demod_shard, S, n, world, rank, dev,
+                          host_collectives=args.dist_backend != "nccl")
+    rec["streams_per_rank"] = S
+    demod.close()
+    torch.cuda.set_stream(torch.cuda.default_stream(dev))
+    torch.cuda.empty_cache()
+    return rec
+
+
+def spawn_ranks(args):
+    """--gpus N without a launcher: run N ranks under torch.distributed.run in a
+    child process (this process never touches the GPU) and return its status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
+                    help="headline workload (default C3, the largest single-GPU config)")
+    ap.add_argument("--sub-configs", default="auto",
+                    help="comma list run after the headline as sub_records; 'auto' = c2,c5 at N=1, "
+                         "c4 at N>1; 'none' = headline only")
+    ap.add_argument("--sub-steps", type=int, default=5)
+    ap.add_argument("--samples", type=int, default=1 << 20)
+    ap.add_argument("--loop-variant", type=int, default=0,
+                    help="symbol-loop kernel shape (qpsk_demod_params.loop_variant; 0 = auto)")
+    ap.add_argument("--streams", type=int, default=0, help="override streams per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="default: os.cpu_count()")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="CPU-time budget per config (x effective cores) of the oracle leg")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo + --share-gpu rehearses the N>1 path on a one-GPU box")
+    ap.add_argument("--timed-only", action="store_true",
+                    help="warmup + timed steps of the headline only (no parity, BER, framer, "
+                         "split/gather, host ring, CPU baseline, sub-records): the command rocprofv3 "
+                         "traces, so its kernel averages are the timed region's")
+    ap.add_argument("--no-host-ring", action="store_true",
+                    help="skip the PCIe-inclusive host-ring pass (N=1, batches <= 4 GiB: C2)")
+    ap.add_argument("--no-framer", action="store_true",
+                    help="skip the device TSC + framer pass measured beside the headline")
+    ap.add_argument("--no-split-gather", action="store_true",
+                    help="skip the RCCL scatter/demod/gather pass that runs when N > 1")
+    ap.add_argument("--serial-calls", action="store_true",
+                    help="synchronous process() per step (no front/back stage overlap)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="every rank uses cuda:0 (rehearsal only; numbers meaningless)")
+    args = ap.parse_args()
+    if args.timed_only:
+        args.no_parity = args.no_framer = args.no_split_gather = True
+        args.no_host_ring = args.no_cpu_baseline = True
+        args.sub_configs = "none"
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
+
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    local = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+
+    out = run_config(args.config, args, rank, world, dev, args.steps, args.warmup, headline=True)
+    subs = args.sub_configs
+    if subs == "auto":
+        subs = "c2,c5" if world == 1 else "c4"
+    sub = {}
+    for key in [k for k in subs.split(",") if k and k != "none" and k != args.config]:
+        r = run_config(key, args, rank, world, dev, args.sub_steps, 1, headline=False)
+        for k in ("metric", "unit", "n_gpus", "higher_is_better", "scaling", "vs_baseline", "dtype"):
+            r.pop(k, None)
+        sub[key] = r
+    if sub:
+        out["sub_records"] = sub
+    if world > 1 and not args.no_split_gather:
+        out["split_gather"] = split_gather_leg(args, rank, world, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    demod.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -35,8 +35,20 @@ extern "C" {
 #define QPSK_ERR_ARGUMENT_NULL (-2)   /* ArgumentNullException (QPSKDeModulator.cs:341,429) */
 #define QPSK_ERR_OUT_OF_RANGE (-3)    /* ArgumentOutOfRangeException (Band-Edge Filter.cs:42-45) */
 #define QPSK_ERR_DEVICE (-4)          /* HIP runtime failure */
-#define QPSK_ERR_CAPACITY (-5)        /* call larger than the handle's max_samples_per_call */
-#define QPSK_ERR_STATE (-6)           /* symbol-sync carry buffer overflow */
+#define QPSK_ERR_CAPACITY (-5)        /* an output row would have been truncated */
+#define QPSK_ERR_STATE (-6)           /* loop state left the reference's defined behaviour
+                                         (QPSK_STATUS_CARRY_OVERFLOW / _NONFINITE_TIMING), or a
+                                         host ring used out of order */
+
+/* status flags (qpsk_demod_status; a host-memory process() call returns the
+ * matching error code when its own call raised one) */
+#define QPSK_STATUS_CARRY_OVERFLOW 1u    /* symbol-sync queue kept > 64 samples (sps > 60):
+                                            the reference keeps them all (MuellerMuller.cs:123-133) */
+#define QPSK_STATUS_OUTPUT_TRUNCATED 2u  /* a bit / symbol row hit its capacity */
+#define QPSK_STATUS_NONFINITE_TIMING 4u  /* a NaN/Inf sample reached the M&M timing loop: the
+                                            reference's (int)Math.Floor(NaN) = 0 pins baseIndex
+                                            at 0 (MuellerMuller.cs:113-115) and its outputs are
+                                            no longer tracked */
 
 /* where a pointer lives */
 #define QPSK_MEM_HOST 0
@@ -61,7 +73,9 @@ typedef struct qpsk_demod_params {
     int32_t vector_lanes;           /* Vector<float>.Count whose summation order the FIR
                                        reproduces: 8 (x64 AVX2, default), 4 (ARM64), 1 (no SIMD) */
     int32_t device;                 /* HIP device ordinal                               */
-    int64_t max_samples_per_call;   /* complex samples per stream per call (device buffers) */
+    int64_t max_samples_per_call;   /* complex samples per stream per internal chunk (device
+                                       buffers), 1 .. 2^30; longer calls run as consecutive
+                                       chunks with identical results */
     int32_t loop_variant;           /* symbol-loop kernel shape: 0 = auto,
                                        1 = 16 streams x 64-sample rounds, 2 = 32 x 64,
                                        3 = 16 x 128 (sps >= 2 only); results are identical */
@@ -96,6 +110,12 @@ int qpsk_demod_set_stream(qpsk_demod *h, void *hip_stream);
  * n_syms    [n_streams] symbol counts or NULL
  * mem       QPSK_MEM_HOST or QPSK_MEM_DEVICE for every pointer above
  * The call is synchronous for host pointers and stream-ordered for device ones.
+ * Any length is accepted (QPSKDeModulator.cs:345-360 takes any span): a call
+ * longer than max_samples_per_call runs as consecutive internal chunks whose
+ * rows are concatenated, bit for bit what one call returns.  Host-memory calls
+ * return QPSK_ERR_STATE / QPSK_ERR_CAPACITY when they raised a QPSK_STATUS_*
+ * flag (outputs are still written); device-memory calls report them through
+ * qpsk_demod_status.
  */
 int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t stride_floats,
                        int64_t n_samples, const int64_t *lengths, int32_t mem, uint8_t *bits,
@@ -121,6 +141,18 @@ int qpsk_demod_process_async(qpsk_demod *h, int32_t mode, const float *iq, int64
                              int64_t n_samples, const int64_t *lengths, uint8_t *bits,
                              int64_t bits_stride_bytes, int64_t *n_bits, float *syms,
                              int64_t syms_stride_floats, int64_t *n_syms);
+/* OR of the QPSK_STATUS_* flags raised since the last qpsk_demod_status call
+ * (waits for every queued call), then cleared.  0 = every call so far stayed
+ * inside the reference's defined behaviour. */
+int qpsk_demod_status(qpsk_demod *h, uint32_t *flags);
+
+/* The matched-filter output (ComplexFIRFilter.Filter, FIRFilter.cs:80-91) of
+ * the last synchronous qpsk_demod_process call of at most max_samples_per_call
+ * samples: n_samples per stream into out [S][stride_floats] (host or device
+ * memory).  For inspection and FIR parity checks; pipelined and chunked calls
+ * leave other buffers behind. */
+int qpsk_demod_last_mf(qpsk_demod *h, float *out, int64_t stride_floats, int64_t n_samples, int32_t mem);
+
 /* Make hip_stream wait for every pipelined call issued so far (NULL: block the
  * calling host thread until they are done). */
 int qpsk_demod_pipeline_wait(qpsk_demod *h, void *hip_stream);
@@ -265,7 +297,8 @@ int qpsk_tsc_find_device(const uint8_t *bits, int64_t bits_stride_bytes, const i
  * splitmix64(seed ^ s); tx_bits receives the payload bits (packed MSB-first).
  * cfo_hz: per-stream carrier offset drawn U[-cfo_hz, +cfo_hz] (0 = clean
  * ±ppm LO pair), multipath: 4-tap channel [1, .25e^{j.7}, .1e^{-j1.9}, .05],
- * esn0_db: AWGN Es/N0 (>= 200 = none).
+ * esn0_db: AWGN Es/N0 (>= 200 = none).  lo_ppm = cfo_hz = 0: no carrier at
+ * all, i.e. QPSKModulator.Modulate's own baseband (QPSKModulator.cs:104-167).
  */
 typedef struct qpsk_synth_params {
     int32_t sample_rate, symbol_rate;
@@ -285,6 +318,51 @@ void qpsk_synth_params_init(qpsk_synth_params *p, int32_t sample_rate, int32_t s
 int qpsk_synth_generate(const qpsk_synth_params *p, int32_t device, void *hip_stream,
                         int32_t n_streams, int64_t n_samples, float *iq_dev,
                         int64_t stride_floats, uint8_t *tx_bits_dev, int64_t bits_stride_bytes);
+
+/* ---------------------------------------------------------------------------
+ * QPSKModulator (QPSKModulator.cs:18-167) behind the same ABI, batched: one
+ * handle = one constructor (RRC taps, TSC, differential flag), one call =
+ * Modulate (or ModulateBytes) on S independent bit strings, computed on the
+ * GPU.  The impulse train (symbol d at delay + d*sps, delay = (T-1)/2) is
+ * filtered by the float RRC taps in double and rounded to float, i.e.
+ * fftFilter's output (FIRFilter.cs:96-141) restated as direct convolution;
+ * output length = delay + nDibits*sps (+ delay when pulse shaping).
+ * ModulateTextUtf8 (:74-89) is ModulateBytes on Encoding.GetBytes results and
+ * stays in the C# shim.
+ */
+typedef struct qpsk_mod_params {
+    int32_t sample_rate;        /* int SampleRate                 */
+    int32_t symbol_rate;        /* int SymbolRate                 */
+    double rrc_alpha;           /* double RrcAlpha = 0.9          */
+    int32_t rrc_span;           /* int rrcSpan = 6                */
+    int32_t differential;       /* bool differentialEncoding = true */
+    int32_t device;             /* HIP device ordinal             */
+    int32_t reserved[7];
+} qpsk_mod_params;
+typedef struct qpsk_mod qpsk_mod;
+void qpsk_mod_params_init(qpsk_mod_params *p, int32_t sample_rate, int32_t symbol_rate);
+/* new QPSKModulator(..., tsc): tsc is a '0'/'1' string prepended to every
+ * Modulate call's data (NULL or blank = none, string.IsNullOrWhiteSpace). */
+int qpsk_mod_create(const qpsk_mod_params *p, const char *tsc, qpsk_mod **out);
+int qpsk_mod_destroy(qpsk_mod *m);
+int qpsk_mod_set_stream(qpsk_mod *m, void *hip_stream);
+/* floats one row of Modulate output holds for n_bits payload bits */
+int64_t qpsk_mod_output_floats(const qpsk_mod *m, int64_t n_bits, int32_t pulse_shaping);
+/* Modulate(string data, bool pulseShaping) on every stream: bits [S][stride]
+ * packed MSB-first (bit i of the string = bit 7 - i%8 of byte i/8), n_bits[s]
+ * bits each (an odd count drops the last bit, :113); out [S][out_stride]
+ * interleaved float, n_out_floats[s] = its length (0 for < 2 bits in all).
+ * mem applies to bits, n_bits, out and n_out_floats. */
+int qpsk_mod_modulate(qpsk_mod *m, int32_t n_streams, const uint8_t *bits, int64_t bits_stride_bytes,
+                      const int64_t *n_bits, int32_t pulse_shaping, int32_t mem, float *out,
+                      int64_t out_stride_floats, int64_t *n_out_floats);
+/* ModulateBytes(payload, startMarker, endMarker, pulseShaping) (:54-72) on every
+ * stream, host memory: payload [S][payload_stride] bytes, n_payload[s] each.
+ * Empty markers are QPSK_ERR_ARGUMENT (ArgumentException, :60-61). */
+int qpsk_mod_modulate_bytes(qpsk_mod *m, int32_t n_streams, const uint8_t *payload, int64_t payload_stride,
+                            const int64_t *n_payload, const uint8_t *start_marker, int32_t n_start,
+                            const uint8_t *end_marker, int32_t n_end, int32_t pulse_shaping, float *out,
+                            int64_t out_stride_floats, int64_t *n_out_floats);
 
 const char *qpsk_last_error(void);
 int qpsk_abi_version(void);

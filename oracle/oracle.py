@@ -110,6 +110,10 @@ def lib():
         L.or_demod_batch.argtypes = [C.POINTER(DemodCfg), C.c_int, _f32p, C.c_long, C.c_long,
                                      C.c_char_p, C.c_long, _i64p, C.c_int]
         L.or_demod_batch.restype = C.c_int
+        L.or_demod_batch_packed.argtypes = [C.POINTER(DemodCfg), C.c_int, _f32p, C.c_long, C.c_long,
+                                            C.c_void_p, C.c_long, C.c_void_p, C.c_void_p, C.c_long,
+                                            C.c_void_p, C.c_int]
+        L.or_demod_batch_packed.restype = C.c_int
         L.or_modulate.argtypes = [C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, C.c_char_p,
                                   C.c_char_p, C.c_long, C.c_int, _f32p, C.c_long]
         L.or_modulate.restype = C.c_long
@@ -241,6 +245,18 @@ def demod_cfg(sample_rate, symbol_rate, rrc_alpha=0.9, rrc_span=6, symbol_sync_b
     return c
 
 
+ERR_INDEX = -3   # OR_ERR_INDEX
+
+
+def _raise(n):
+    """The C# exception a negative oracle return stands for."""
+    if n == -1:
+        raise ValueError("Samples must be interleaved IQ with even length.")
+    if n == ERR_INDEX:
+        raise IndexError("IndexOutOfRangeException: NaN symbol timing pinned baseIndex at 0 "
+                         "(MuellerMuller.cs:113-115, 164)")
+
+
 class OracleDemod:
     """QPSKDeModulator restated (QPSKDeModulator.cs:11-457)."""
 
@@ -263,8 +279,7 @@ class OracleDemod:
         cap = iq.size + 16
         buf = C.create_string_buffer(cap)
         n = lib().or_demod_demodulate(self._h, _fp(iq), iq.size, buf, cap)
-        if n < 0:
-            raise ValueError("Samples must be interleaved IQ with even length.")
+        _raise(n)
         return buf.raw[:n].decode()
 
     def demodulate_ex(self, iq):
@@ -276,16 +291,14 @@ class OracleDemod:
         ns, ti = C.c_long(), C.c_long()
         n = lib().or_demod_demodulate_ex(self._h, _fp(iq), iq.size, buf, cap, _fp(syms), syms.size,
                                          C.byref(ns), C.byref(ti))
-        if n < 0:
-            raise ValueError("Samples must be interleaved IQ with even length.")
+        _raise(n)
         return buf.raw[:n].decode(), syms[: 2 * ns.value].copy(), ti.value
 
     def deModulateConstellation(self, iq):
         iq = _f32(iq)
         out = np.zeros(max(iq.size, 2), dtype=np.float32)
         n = lib().or_demod_constellation(self._h, _fp(iq), iq.size, _fp(out), out.size)
-        if n < 0:
-            raise ValueError("Samples must be interleaved IQ with even length.")
+        _raise(n)
         return out[: 2 * n].copy()
 
     def DeModulateBytes(self, iq, start: bytes, end: bytes) -> bytes:
@@ -300,8 +313,7 @@ class OracleDemod:
         out = np.zeros(cap, dtype=np.uint8)
         n = lib().or_demod_bytes(self._h, _fp(iq), iq.size, s.ctypes.data_as(_u8p), s.size,
                                  e.ctypes.data_as(_u8p), e.size, out.ctypes.data_as(_u8p), cap)
-        if n == -1:
-            raise ValueError("Samples must be interleaved IQ with even length.")
+        _raise(n)
         return bytes(out[:n])
 
     def DeModulateTextUtf8(self, iq, start="\u0002", end="\u0003") -> str:
@@ -351,6 +363,29 @@ def demod_batch_timed(iq2d, sample_rate, symbol_rate, n_threads=1, **kw):
     if rc:
         raise ValueError("oracle batch failed %d" % rc)
     return nb
+
+
+def demod_batch_packed(iq2d, sample_rate, symbol_rate, n_threads=1, want_bits=True,
+                       want_syms=False, **kw):
+    """One DeModulate call per row of iq2d ([S, 2n] float32) on n_threads host
+    threads.  Returns (bits [S, B] uint8 packed MSB-first like the GPU rows or
+    None, n_bits [S], syms [S, 2n] float32 or None, n_syms [S])."""
+    iq2d = np.ascontiguousarray(iq2d, dtype=np.float32)
+    S, nf = iq2d.shape
+    cfg = demod_cfg(sample_rate, symbol_rate, **kw)
+    bstride = (nf + 7) // 8 + 8
+    bits = np.zeros((S, bstride), dtype=np.uint8) if want_bits else None
+    syms = np.zeros((S, max(nf, 2)), dtype=np.float32) if want_syms else None
+    nb = np.zeros(S, dtype=np.int64)
+    ns = np.zeros(S, dtype=np.int64)
+    rc = lib().or_demod_batch_packed(C.byref(cfg), S, _fp(iq2d), nf, nf,
+                                     bits.ctypes.data if bits is not None else None, bstride,
+                                     nb.ctypes.data, syms.ctypes.data if syms is not None else None,
+                                     syms.shape[1] if syms is not None else 0, ns.ctypes.data,
+                                     int(n_threads))
+    if rc:
+        raise ValueError("oracle batch failed %d" % rc)
+    return bits, nb, syms, ns
 
 
 def modulate(sample_rate, symbol_rate, bits: str, rrc_alpha=0.9, rrc_span=6, differential=True,

@@ -289,13 +289,28 @@ static inline void mm_lagrange(const or_mm *m, long n, double mu, float *oi, flo
     *oq = cm1 * xm1q + c0 * x0q + c1 * x1q + c2 * x2q;
 }
 
-/* :52-136 Process(span) */
+/* (int)d in .NET 9: saturating, NaN -> 0 (x64 conversions were made
+ * saturating in .NET 9; C leaves NaN and out-of-range undefined) */
+static int or_dotnet_int(double d)
+{
+    if (d != d) return 0;
+    if (d >= 2147483647.0) return 2147483647;
+    if (d <= -2147483648.0) return (int)-2147483647 - 1;
+    return (int)d;
+}
+
+/* :52-136 Process(span).  Returns the symbol count, -1 for an odd length, or
+ * OR_ERR_INDEX where the C# indexer would throw IndexOutOfRangeException: a
+ * NaN timing pins baseIndex at (int)Math.Floor(NaN) = 0, and CubicLagrange4
+ * then reads _bufIQ[(_bufStart - 1) * 2] (:164), out of range while
+ * _bufStart == 0. */
 long or_mm_process(or_mm *m, const float *in_iq, long n_floats, float *out_iq, long out_floats)
 {
     if (n_floats & 1) return -1;
     mm_append(m, in_iq, n_floats);
     long out_sym = 0;
     while (m->base + 2 < m->count) {
+        if (m->start + m->base - 1 < 0) return OR_ERR_INDEX;
         float ci, cq;
         mm_lagrange(m, m->base, m->mu, &ci, &cq);
         float di = (ci >= 0.0f) ? 1.0f : -1.0f;                /* :194-198 */
@@ -323,7 +338,7 @@ long or_mm_process(or_mm *m, const float *in_iq, long n_floats, float *out_iq, l
         m->psi = ci; m->psq = cq;
         m->pdi = di; m->pdq = dq;
         double nt = m->base + m->mu + adv;                           /* :113 */
-        m->base = (int)floor(nt);
+        m->base = or_dotnet_int(floor(nt));
         m->mu = nt - m->base;
         if (m->base + 1 >= m->count) break;
     }
@@ -700,6 +715,7 @@ static long demod_core(or_demod *d, const float *iq, long n_floats, char *bits, 
     }
     or_cfir_filter(d->rrc, src, d->tmp_rrc, n_floats >> 1);     /* :360 */
     long nsym = or_mm_process(d->mm, d->tmp_rrc, n_floats, d->tmp_sym, n_floats); /* :364 */
+    if (nsym < 0) return nsym;                                    /* the C# call throws */
     long nb = 0;
     for (long k = 0; k < nsym; k++) {                             /* :372-408 */
         float si = d->tmp_sym[2 * k], sq = d->tmp_sym[2 * k + 1];
@@ -759,6 +775,7 @@ long or_demod_demodulate_ex(or_demod *d, const float *iq, long n_floats, char *b
     if (tsc_idx) *tsc_idx = 0;
     if (n_floats == 0) return 0;                                  /* :350-351 */
     long nb = demod_core(d, iq, n_floats, bits, cap, syms, syms_cap_floats, n_syms);
+    if (nb < 0) return nb;
     if (tsc_idx) *tsc_idx = tsc_start(d, bits, nb < cap ? nb : cap);
     return nb;
 }
@@ -773,6 +790,7 @@ long or_demod_demodulate(or_demod *d, const float *iq, long n_floats, char *bits
         d->bits_cap = need;
     }
     long nb = demod_core(d, iq, n_floats, d->bits, d->bits_cap, NULL, 0, NULL);
+    if (nb < 0) return nb;
     long s = tsc_start(d, d->bits, nb);
     if (s < 0) return 0;
     long n = nb - s;
@@ -792,6 +810,7 @@ long or_demod_constellation(or_demod *d, const float *iq, long n_floats, float *
     }
     or_cfir_filter(d->rrc, src, d->tmp_rrc, n_floats >> 1);
     long nsym = or_mm_process(d->mm, d->tmp_rrc, n_floats, d->tmp_sym, n_floats);
+    if (nsym < 0) return nsym;
     for (long k = 0; k < nsym; k++) {
         float ri, rq;
         or_costas_process(d->costas, d->tmp_sym[2 * k], d->tmp_sym[2 * k + 1], &ri, &rq);
@@ -878,7 +897,7 @@ long or_demod_bytes(or_demod *d, const float *iq, long n_floats, const uint8_t *
     char *rx = (char *)malloc((size_t)need);
     long n_rx = or_demod_demodulate(d, iq, n_floats, rx, need);  /* :178 */
     long result = 0;
-    if (n_rx <= 0) { free(rx); return 0; }
+    if (n_rx <= 0) { free(rx); return n_rx < 0 ? n_rx : 0; }
     if (!d->in_frame) {
         long nc = d->carry_len + n_rx;                            /* :185 */
         char *cand = (char *)malloc((size_t)nc + 1);
@@ -969,6 +988,87 @@ static void *batch_worker(void *arg)
         or_demod_free(d);
     }
     return NULL;
+}
+
+/* Packed variant for the bench's parity-at-scale check and the all-core CPU
+ * baseline: the raw (pre-TSC) bits of one DeModulate call per stream, packed
+ * MSB-first exactly like the GPU bit rows (BitPacker order, HelperFunctions.cs:14-29),
+ * plus optionally the rotated Costas symbols.  Streams are handed out through
+ * an atomic counter (any thread count, no static partition).  bits / syms may
+ * be NULL (timing only). */
+typedef struct {
+    const or_demod_cfg *cfg;
+    const float *iq;
+    long stride, n_floats;
+    uint8_t *bits;
+    long bits_stride;
+    long *n_bits;
+    float *syms;
+    long syms_stride;
+    long *n_syms;
+    int n_streams;
+    int *next;
+    int rc;
+} packed_job;
+
+static void *packed_worker(void *arg)
+{
+    packed_job *j = (packed_job *)arg;
+    char *tmp = (char *)malloc((size_t)j->n_floats + 16);
+    for (;;) {
+        int s = __atomic_fetch_add(j->next, 1, __ATOMIC_RELAXED);
+        if (s >= j->n_streams) break;
+        int err;
+        or_demod *d = or_demod_new(j->cfg, &err);
+        if (!d) { j->rc = err ? err : -1; break; }
+        long ns = 0;
+        float *srow = j->syms ? j->syms + (long)s * j->syms_stride : NULL;
+        long nb = 0;
+        if (j->n_floats > 0)
+            nb = demod_core(d, j->iq + (long)s * j->stride, j->n_floats, tmp, j->n_floats + 16, srow,
+                            j->syms ? j->syms_stride : 0, &ns);
+        if (j->n_bits) j->n_bits[s] = nb;
+        if (j->n_syms) j->n_syms[s] = ns;
+        if (j->bits) {
+            uint8_t *row = j->bits + (long)s * j->bits_stride;
+            long nbytes = (nb + 7) / 8;
+            if (nbytes > j->bits_stride) nbytes = j->bits_stride;
+            memset(row, 0, (size_t)nbytes);
+            for (long i = 0; i < nb && (i >> 3) < nbytes; i++)
+                if (tmp[i] == '1') row[i >> 3] |= (uint8_t)(0x80u >> (i & 7));
+        }
+        or_demod_free(d);
+    }
+    free(tmp);
+    return NULL;
+}
+
+int or_demod_batch_packed(const or_demod_cfg *cfg, int n_streams, const float *iq, long stride_floats,
+                          long n_floats, uint8_t *bits, long bits_stride, long *n_bits, float *syms,
+                          long syms_stride_floats, long *n_syms, int n_threads)
+{
+    if (n_floats & 1) return -1;
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > n_streams) n_threads = n_streams > 0 ? n_streams : 1;
+    pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+    packed_job *jobs = (packed_job *)calloc((size_t)n_threads, sizeof(packed_job));
+    int next = 0;
+    for (int t = 0; t < n_threads; t++) {
+        packed_job *j = &jobs[t];
+        j->cfg = cfg; j->iq = iq; j->stride = stride_floats; j->n_floats = n_floats;
+        j->bits = bits; j->bits_stride = bits_stride; j->n_bits = n_bits;
+        j->syms = syms; j->syms_stride = syms_stride_floats; j->n_syms = n_syms;
+        j->n_streams = n_streams; j->next = &next; j->rc = 0;
+        pthread_create(&th[t], NULL, packed_worker, j);
+    }
+    int rc = 0;
+    for (int t = 0; t < n_threads; t++) {
+        pthread_join(th[t], NULL);
+        if (jobs[t].rc) rc = jobs[t].rc;
+    }
+    free(th);
+    free(jobs);
+    return rc;
 }
 
 int or_demod_batch(const or_demod_cfg *cfg, int n_streams, const float *iq, long stride_floats,

@@ -37,6 +37,8 @@ void or_cfir_filter(or_cfir *f, const float *in_iq, float *out_iq, long n_comple
 
 /* MuellerMuller.cs:17-249 */
 typedef struct or_mm or_mm;
+/* the C# path would throw IndexOutOfRangeException (see or_mm_process) */
+#define OR_ERR_INDEX (-3)
 or_mm *or_mm_new(double sps, double kp, double ki);
 void or_mm_free(or_mm *m);
 long or_mm_process(or_mm *m, const float *in_iq, long n_floats, float *out_iq, long out_floats);
@@ -99,6 +101,11 @@ long or_index_of(const uint8_t *hay, long n_hay, const uint8_t *needle, long n_n
  * one DeModulate call of n_floats.  bits_out is [S][bits_cap] chars. */
 int or_demod_batch(const or_demod_cfg *cfg, int n_streams, const float *iq, long stride_floats,
                    long n_floats, char *bits_out, long bits_cap, long *n_bits, int n_threads);
+/* one DeModulate call per stream, raw bits packed MSB-first into rows of
+ * bits_stride bytes (+ optional rotated symbols); work-stealing threads */
+int or_demod_batch_packed(const or_demod_cfg *cfg, int n_streams, const float *iq, long stride_floats,
+                          long n_floats, uint8_t *bits, long bits_stride, long *n_bits, float *syms,
+                          long syms_stride_floats, long *n_syms, int n_threads);
 
 /* Input synthesis (not accelerated): QPSKModulator.cs:104-167 with the MathNet
  * FFT of FIRFilter.cs:96-141 restated as direct double convolution.

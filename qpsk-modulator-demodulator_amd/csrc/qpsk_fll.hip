@@ -38,7 +38,7 @@
 #include <cstdint>
 
 #include "qpsk_kernels.h"
-#include "qpsk_sincos.h"
+#include "qpsk_sincosf.h"
 
 #ifndef QPSK_FLL_PROBE
 #define QPSK_FLL_PROBE 0   // diagnostic bits (timing only, results wrong): 1 no sincos, 2 no
@@ -54,8 +54,6 @@ constexpr int kRingLen = 64;             // mixed samples per stream: x[t] at t 
 constexpr int kRingRow = 2 * kRingLen + 2;   // +2 entries: a wave's 8 rows hit distinct banks
 
 struct FllSysLds {
-    double tab[1024];                    // sincos table (qpsk_sincos.h)
-    double tab_lo[1024];
     f2 ring[kSysStreams * kRingRow];
     float taps[2 * kFllTaps];            // lower taps, reversed, interleaved (prologue)
 };
@@ -125,10 +123,6 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
     constexpr int N = kFllTaps;
     static_assert(N == 40, "systolic FLL assumes 5 blocks of 8 taps");
     __shared__ FllSysLds L;
-    for (int i = threadIdx.x; i < 1024; i += 256) {
-        L.tab[i] = qpsk_sincos_table_dev[i];
-        L.tab_lo[i] = qpsk_sincos_table_dev_lo[i];
-    }
     if (threadIdx.x < 2 * N) L.taps[threadIdx.x] = P.lower_rev[threadIdx.x];
 
     const int lane = threadIdx.x & 63;
@@ -215,9 +209,6 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
 
     const float two_pi = 2.0f * 3.14159274101257324219f;
     const float beta = P.beta, alpha = P.alpha, fmax_ = P.max_freq, fmin_ = P.min_freq;
-    qpsk_sincos_consts K = QPSK_SINCOS_CONSTS_INIT;
-    asm volatile("" : "+v"(K.INV), "+v"(K.SH), "+v"(K.P1), "+v"(K.P2), "+v"(K.P3));
-    asm volatile("" : "+v"(K.S3), "+v"(K.S5), "+v"(K.C4), "+v"(K.C6));
 
     // one sample (Band-Edge Filter.cs:102-129) at t = t0 + u, t0 a multiple of 8.
     // FIRST: the call's first sample (the stored phase may be anything set_state
@@ -228,20 +219,18 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
     // so a block is branch-free straight-line code.
     auto step = [&](f2 in, int64_t t0, int u, auto first, auto exact, float &amax, float &fmx)
         __attribute__((always_inline)) {
+        // MathF.Cos / MathF.Sin (Band-Edge Filter.cs:108-109) = glibc cosf / sinf
         float sn, cs;
         if constexpr (decltype(first)::value) {
-            qpsk_sincosf_tab(phase, L.tab, L.tab_lo, &sn, &cs);
+            qpsk_sincosf_glibc(phase, &sn, &cs);
 #if QPSK_FLL_PROBE & 1
         } else if (true) {   // diagnostic: no sincos on the chain
             sn = phase * 0.5f;
             cs = 1.0f - phase;
 #endif
         } else {
-            // a kept result has |phase| <= 2pi (or NaN): the float-argument core
-            double sd, cd;
-            qpsk_sincos_tab_core_f(static_cast<double>(phase), L.tab, L.tab_lo, &K, &sd, &cd);
-            sn = static_cast<float>(sd);
-            cs = static_cast<float>(cd);
+            // a kept result has |phase| <= 2pi (or NaN): the branch-free form
+            qpsk_sincosf_glibc_fast(phase, &sn, &cs);
         }
         const f2 csn = f2{cs, sn};
         // (inI*c - inQ*s, inI*s + inQ*c)

@@ -44,6 +44,25 @@ struct LoopArgs {
     int64_t *n_syms;
     int S;
     unsigned long long *probe;   // diagnostic cycle stamps (QPSK_LOOP_STAMPS builds only)
+    uint32_t *flags;       // per-handle OR of QPSK_STATUS_* raised by this call (or nullptr)
+};
+
+// One internal chunk's rows appended behind what earlier chunks of the same
+// call wrote: bits at per-stream bit offsets acc[s], symbols at acc[S + s]
+// (first = the call's first chunk: offsets 0).
+struct AppendArgs {
+    uint8_t *dst_bits;           // [S][dst_bits_stride] or nullptr
+    int64_t dst_bits_stride;     // bytes
+    float *dst_syms;             // [S][dst_syms_stride] interleaved or nullptr
+    int64_t dst_syms_stride;     // floats
+    const uint32_t *src_bits;    // [S][src_bits_words] (MSB-first bytes)
+    int64_t src_bits_words;
+    const float *src_syms;       // [S][2 * src_syms_cap]
+    int64_t src_syms_cap;
+    const int64_t *counts;       // [2][S]: this chunk's n_bits, n_syms
+    int64_t *acc;                // [2][S]: running totals
+    int first;
+    int S;
 };
 
 struct FllArgs {
@@ -64,6 +83,7 @@ bool launch_fir(const FirArgs &a, const TapsRev &taps, const float *hrev_dev, in
 void launch_fir_hist(const FirArgs &a, float *hist_new, int H, int S, hipStream_t stream);
 void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant,
                  hipStream_t stream);
+void launch_append(const AppendArgs &a, hipStream_t stream);
 void launch_fll(const FllArgs &a, const FllParams &P, hipStream_t stream);
 void launch_fll_sys(const FllArgs &a, const FllParams &P, hipStream_t stream);   // qpsk_fll.hip
 

@@ -41,6 +41,42 @@ constexpr int lds_slots(int n) { return n + ((n >> 6) << 3) + 8; }
 
 constexpr int kFirThreads = 256;
 
+// One output of the tile with the reference's full complex products
+// (FIRFilter.cs:165-192): lane accumulators from +0, (hI*xI) - (hQ*xQ) and
+// (hI*xQ) + (hQ*xI) with hQ = +0 (the RRC's imaginary taps).  The fast path
+// drops the hQ products, which is exact for finite samples; a NaN or Inf
+// sample makes 0*x NaN, so tiles whose fast outputs are not all finite are
+// recomputed here.  x(k) = window sample k (oldest first) from LDS.
+// Rolled loops (inlined into the rare branch): few registers, so the fast
+// path's allocation is unchanged.
+template <typename XF>
+__device__ __forceinline__ f2 fir_exact_one(XF x, const float *hrev, int T, int W) {
+    const float hq = 0.0f;
+    float ai = 0.0f, aq = 0.0f;
+    const int nvec = W > 1 ? T - T % W : 0;
+#pragma unroll 1
+    for (int l = 0; l < (W > 1 ? W : 0); ++l) {
+        float vi = 0.0f, vq = 0.0f;
+#pragma unroll 1
+        for (int k = l; k < nvec; k += W) {
+            const f2 u = x(k);
+            const float hi = hrev[k];
+            vi = vi + ((hi * u.x) - (hq * u.y));
+            vq = vq + ((hi * u.y) + (hq * u.x));
+        }
+        ai += vi;
+        aq += vq;
+    }
+#pragma unroll 1
+    for (int k = nvec; k < T; ++k) {
+        const f2 u = x(k);
+        const float hi = hrev[k];
+        ai += (hi * u.x) - (hq * u.y);
+        aq += (hi * u.y) + (hq * u.x);
+    }
+    return f2{ai, aq};
+}
+
 template <int T, int W, int Q, bool VEC>
 __global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRev taps, const float *hrev) {
     constexpr int TILE = kFirThreads * Q;
@@ -153,24 +189,49 @@ __global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRe
     for (int q = 0; q < Q; ++q) lds[72 * grp + r + W * q] = acc[q];
     __syncthreads();
 
+    // A NaN or Inf sample anywhere in the tile (halo included) leaves some
+    // fast output non-finite; the stores below watch for that, and such a tile
+    // is recomputed with the reference's full products straight from HBM.
+    int bad = 0;
+    auto nonfinite = [](float v) -> int { return __builtin_amdgcn_classf(v, 0x207); };   // NaN, +-Inf
     f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride + a.y_offset;
     if constexpr (VEC) {
         for (int p = tid; p < TILE / 2; p += kFirThreads) {
             const int64_t g = tile0 + 2 * p;
+            const f4 v = *reinterpret_cast<const f4 *>(&lds[lds_slot(2 * p)]);
+            bad |= nonfinite(v.x) | nonfinite(v.y) | nonfinite(v.z) | nonfinite(v.w);
             if (g + 1 < n) {
-                *reinterpret_cast<f4 *>(y + g) = *reinterpret_cast<const f4 *>(&lds[lds_slot(2 * p)]);
+                *reinterpret_cast<f4 *>(y + g) = v;
             } else if (g < n) {
-                y[g] = lds[lds_slot(2 * p)];
+                y[g] = f2{v.x, v.y};
             }
         }
     } else {
         for (int i = tid; i < TILE; i += kFirThreads) {
             const int64_t g = tile0 + i;
-            if (g < n) y[g] = lds[lds_slot(i)];
+            const f2 v = lds[lds_slot(i)];
+            bad |= nonfinite(v.x) | nonfinite(v.y);
+            if (g < n) y[g] = v;
+        }
+    }
+    if (__syncthreads_or(bad)) {
+        const int o0 = 64 * (tid / W) + tid % W;
+#pragma unroll 1
+        for (int q = 0; q < Q; ++q) {
+            const int64_t go = tile0 + o0 + W * q;       // output sample
+            if (go >= n) continue;
+            const int64_t w0 = go - (T - 1);             // its oldest window sample
+            auto xs = [&](int k) -> f2 {
+                const int64_t g = w0 + k;
+                return g < 0 ? hist[T - 1 + g] : x[g];
+            };
+            y[go] = fir_exact_one(xs, hrev, T, W);
         }
     }
 }
 
+// Any (T, W) without a specialised tile kernel: the reference's formula
+// itself, full complex products included (not on the benchmarked path).
 __global__ __launch_bounds__(256) void fir_generic_kernel(FirArgs a, const float *hrev, int T,
                                                           int W) {
     const int s = blockIdx.y;
@@ -179,22 +240,13 @@ __global__ __launch_bounds__(256) void fir_generic_kernel(FirArgs a, const float
     if (t >= n) return;
     const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
     const f2 *hist = reinterpret_cast<const f2 *>(a.hist) + static_cast<int64_t>(s) * (T - 1);
-    auto X = [&](int64_t g) -> f2 { return g < 0 ? hist[T - 1 + g] : x[g]; };
     const int64_t w0 = t - T + 1;
-    f2 acc = f2{0.f, 0.f};
-    if (W > 1) {
-        const int nvec = T - T % W;
-        for (int l = 0; l < W; ++l) {
-            f2 A = f2{0.f, 0.f};
-            for (int i = 0; i < nvec; i += W) A = A + hrev[i + l] * X(w0 + i + l);
-            acc = acc + A;
-        }
-        for (int i = nvec; i < T; ++i) acc = acc + hrev[i] * X(w0 + i);
-    } else {
-        for (int i = 0; i < T; ++i) acc = acc + hrev[i] * X(w0 + i);
-    }
+    auto xs = [&](int k) -> f2 {
+        const int64_t g = w0 + k;
+        return g < 0 ? hist[T - 1 + g] : x[g];
+    };
     f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride + a.y_offset;
-    y[t] = acc;
+    y[t] = fir_exact_one(xs, hrev, T, W);
 }
 
 // new_hist = last (T-1) samples of concat(old_hist, x[0..n))
@@ -250,13 +302,6 @@ __device__ __forceinline__ void fll_dot(const float *taps_rev, const f2 *win, in
 }
 
 __global__ __launch_bounds__(64) void fll_kernel(FllArgs a, FllParams P) {
-    __shared__ double tab[1024];
-    __shared__ double tab_lo[1024];
-    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
-        tab[i] = qpsk_sincos_table_dev[i];
-        tab_lo[i] = qpsk_sincos_table_dev_lo[i];
-    }
-    __syncthreads();
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= a.S) return;
     const int64_t n = a.lengths ? a.lengths[s] : a.n;
@@ -274,7 +319,7 @@ __global__ __launch_bounds__(64) void fll_kernel(FllArgs a, FllParams P) {
     for (int64_t t = 0; t < n; ++t) {
         const f2 in = x[t];
         float sn, cs;
-        qpsk_sincosf_tab(phase, tab, tab_lo, &sn, &cs);
+        qpsk_sincosf_glibc(phase, &sn, &cs);   // MathF.Cos/Sin = glibc (Band-Edge Filter.cs:108-109)
         const float oi = in.x * cs - in.y * sn;
         const float oq = in.x * sn + in.y * cs;
         y[t] = f2{oi, oq};
@@ -301,6 +346,57 @@ __global__ __launch_bounds__(64) void fll_kernel(FllArgs a, FllParams P) {
     a.state[s].fll_phase = phase;
     a.state[s].fll_freq = freq;
     a.state[s].fll_pos = pos;
+}
+
+// ---------------------------------------------------------------------------
+// Chunked calls: one DeModulate call longer than max_samples_per_call runs as
+// consecutive internal chunks (the chain is chunk-invariant), and each chunk's
+// bit row / symbol row is appended behind the previous chunk's in the
+// caller's row, so the caller sees one call's output (QPSKDeModulator.cs:345-425
+// takes any span length).  One workgroup per stream.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void append_rows_kernel(AppendArgs a) {
+    const int s = blockIdx.x;
+    const int64_t nb = a.counts[s], ns = a.counts[a.S + s];
+    const int64_t off = a.first ? 0 : a.acc[s];
+    const int64_t offs = a.first ? 0 : a.acc[a.S + s];
+    if (a.dst_bits && nb > 0) {
+        // dst bit off + i <- src bit i, MSB-first: dst byte base + j takes the
+        // low sh bits of src byte j-1 and the high 8-sh bits of src byte j
+        const uint8_t *src = reinterpret_cast<const uint8_t *>(a.src_bits + s * a.src_bits_words);
+        uint8_t *dst = a.dst_bits + s * a.dst_bits_stride;
+        const int sh = static_cast<int>(off & 7);
+        const int64_t base = off >> 3;
+        const int64_t nsrc = (nb + 7) >> 3;
+        const int64_t nout = ((off + nb + 7) >> 3) - base;
+        for (int64_t j = threadIdx.x; j < nout; j += blockDim.x) {
+            const unsigned cur = j < nsrc ? src[j] : 0u;
+            const unsigned prev = j > 0 ? src[j - 1] : 0u;
+            unsigned v = ((prev << (8 - sh)) | (cur >> sh)) & 0xffu;
+            if (j == 0 && sh) v |= dst[base] & (0xff00u >> sh);   // earlier chunk's bits
+            // bits past the end of this chunk are zero in src (the loop kernel
+            // pads the last word with zeros); mask them anyway
+            if (j == nout - 1) {
+                const int tail = static_cast<int>((off + nb) & 7);
+                if (tail) v &= 0xff00u >> tail;
+            }
+            dst[base + j] = static_cast<uint8_t>(v);
+        }
+    }
+    if (a.dst_syms && ns > 0) {
+        const float *src = a.src_syms + s * 2 * a.src_syms_cap;
+        float *dst = a.dst_syms + s * a.dst_syms_stride + 2 * offs;
+        for (int64_t i = threadIdx.x; i < 2 * ns; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();   // every thread has read acc
+    if (threadIdx.x == 0) {
+        a.acc[s] = off + nb;
+        a.acc[a.S + s] = offs + ns;
+    }
+}
+
+void launch_append(const AppendArgs &a, hipStream_t stream) {
+    hipLaunchKernelGGL(append_rows_kernel, dim3(a.S), dim3(256), 0, stream, a);
 }
 
 // ---------------------------------------------------------------------------

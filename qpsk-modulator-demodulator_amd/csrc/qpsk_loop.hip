@@ -536,9 +536,16 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         int keep = count - consumed;
         if (keep > kCarryMax) {
             atomicOr(&a.state[s].error, 1);
+            if (a.flags) atomicOr(a.flags, 1u);
             consumed = count - kCarryMax;
             keep = kCarryMax;
         }
+        // a non-finite sample that reached the timing loop leaves the PI
+        // integrator NaN: the reference's correction, and with it newTime, go
+        // NaN, and (int)Math.Floor(NaN) = 0 (.NET 9 saturating conversion) pins
+        // baseIndex at 0 from then on (MuellerMuller.cs:83-115).  This kernel
+        // clamps the NaN correction instead; the call is flagged either way.
+        if (!(integ == integ) && a.flags) atomicOr(a.flags, 4u);
         const f2 *q = reinterpret_cast<const f2 *>(a.mf) + s * a.mf_stride + kMfPrefix - R;  // logical 0
         f2 *cw = reinterpret_cast<f2 *>(a.carry) + static_cast<int64_t>(s) * kCarryMax;
         for (int i = 0; i < keep; ++i) cw[i] = q[consumed + i];
@@ -776,7 +783,10 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         g->diff_pi = dpi;
         g->diff_pq = dpq;
     }
-    if (err) atomicOr(&g->error, err);
+    if (err) {
+        atomicOr(&g->error, err);
+        if (a.flags) atomicOr(a.flags, static_cast<uint32_t>(err));
+    }
     if (a.n_bits) a.n_bits[s] = MODE == kModeDemodulate ? nbits : 0;
 }
 

@@ -71,6 +71,7 @@ int dev_alloc(T **p, size_t count) {
 }
 
 constexpr int kEv = 6;
+constexpr int64_t kMaxSamplesPerCall = int64_t(1) << 30;
 }  // namespace
 
 namespace qpsk {
@@ -108,6 +109,19 @@ struct qpsk_demod {
     int64_t *d_counts = nullptr;     // [2][S]: n_bits, n_syms
     int64_t *d_lengths[2] = {nullptr, nullptr};
     int64_t *h_counts = nullptr;     // pinned
+    // status flags (QPSK_STATUS_*): [0] = raised by device-memory calls since the
+    // last qpsk_demod_status, [1] = raised by the current host-memory call
+    uint32_t *d_flags = nullptr;
+    uint32_t *h_flags = nullptr;     // pinned
+    uint32_t status_host = 0;        // raised by host-memory calls since the last status
+    // chunked calls (longer than max_samples_per_call): running per-stream
+    // output offsets [2][S] and, for host-memory calls, device staging of the
+    // whole call's output rows
+    int64_t *d_acc = nullptr;
+    uint8_t *d_xbits = nullptr;
+    size_t xbits_bytes = 0;
+    float *d_xsyms = nullptr;
+    size_t xsyms_bytes = 0;
     bool timing = false;
     // one set of kEv events per timed call (start, FLL end, FIR start, FIR end,
     // loop start, loop end), each on the stream its stage runs on; averaged by
@@ -161,6 +175,15 @@ struct Call {
     int64_t *n_syms;
     int64_t n_call = 0;    // derived by validate()
     int64_t max_sym = 0;
+    // internal chunk of a longer call: outputs appended to dst_* at the running
+    // offsets d_acc (first chunk: from 0), totals to n_bits / n_syms after the last
+    bool append = false, first = false, last = false;
+    uint8_t *dst_bits = nullptr;
+    int64_t dst_bits_stride = 0;
+    float *dst_syms = nullptr;
+    int64_t dst_syms_stride = 0;
+    int64_t *dst_n_bits = nullptr;   // device; written after the last chunk
+    int64_t *dst_n_syms = nullptr;
 };
 
 int validate(qpsk_demod *h, Call &c) {
@@ -179,7 +202,6 @@ int validate(qpsk_demod *h, Call &c) {
         if (c.n_samples < 0) return fail(QPSK_ERR_ARGUMENT, "negative n_samples");
         n_call = c.n_samples;
     }
-    if (n_call > h->n_max) return fail(QPSK_ERR_CAPACITY, "call longer than max_samples_per_call");
     if (n_call > 0 && !c.iq) return fail(QPSK_ERR_ARGUMENT_NULL, "SamplesIQ is null");
     if (n_call > 0 && c.stride_floats < 2 * n_call) return fail(QPSK_ERR_ARGUMENT, "stride too small");
     if (c.mode == QPSK_MODE_DEMODULATE && (!c.bits || !c.n_bits))
@@ -278,9 +300,34 @@ int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipS
     la.syms_cap = h->syms_cap;
     la.n_syms = h->d_counts + S;
     la.S = S;
+    la.flags = h->d_flags + (c.mem == QPSK_MEM_HOST && !c.append ? 1 : 0);
     launch_loop(la, h->lp, c.mode, h->loop_variant, st);
     HIP_TRY(hipGetLastError());
     EV(5, st);
+    if (c.append) {
+        AppendArgs aa{};
+        aa.dst_bits = c.mode == QPSK_MODE_DEMODULATE ? c.dst_bits : nullptr;
+        aa.dst_bits_stride = c.dst_bits_stride;
+        aa.dst_syms = c.syms ? c.dst_syms : nullptr;
+        aa.dst_syms_stride = c.dst_syms_stride;
+        aa.src_bits = h->d_bits;
+        aa.src_bits_words = h->bits_words;
+        aa.src_syms = h->d_syms;
+        aa.src_syms_cap = h->syms_cap;
+        aa.counts = h->d_counts;
+        aa.acc = h->d_acc;
+        aa.first = c.first ? 1 : 0;
+        aa.S = S;
+        launch_append(aa, st);
+        HIP_TRY(hipGetLastError());
+        if (c.last) {
+            if (c.dst_n_bits)
+                HIP_TRY(hipMemcpyAsync(c.dst_n_bits, h->d_acc, S * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+            if (c.dst_n_syms)
+                HIP_TRY(hipMemcpyAsync(c.dst_n_syms, h->d_acc + S, S * sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+        }
+        return QPSK_OK;
+    }
     const hipMemcpyKind kind = c.mem == QPSK_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
     const int64_t bytes_row = (2 * c.max_sym + 7) / 8;
     if (c.bits && bytes_row > 0)
@@ -290,9 +337,11 @@ int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipS
                                  2 * h->syms_cap * sizeof(float), 2 * c.max_sym * sizeof(float), S, kind, st));
     if (c.mem == QPSK_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(h->h_counts, h->d_counts, 2 * S * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(h->h_flags, h->d_flags + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         if (c.n_bits) std::memcpy(c.n_bits, h->h_counts, S * sizeof(int64_t));
         if (c.n_syms) std::memcpy(c.n_syms, h->h_counts + S, S * sizeof(int64_t));
+        h->status_host |= *h->h_flags;
     } else {
         if (c.n_bits) HIP_TRY(hipMemcpyAsync(c.n_bits, h->d_counts, S * sizeof(int64_t), kind, st));
         if (c.n_syms) HIP_TRY(hipMemcpyAsync(c.n_syms, h->d_counts + S, S * sizeof(int64_t), kind, st));
@@ -382,6 +431,11 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
     *out = nullptr;
     if (n_streams <= 0) return fail(QPSK_ERR_ARGUMENT, "n_streams must be positive");
     if (p->max_samples_per_call <= 0) return fail(QPSK_ERR_ARGUMENT, "max_samples_per_call must be positive");
+    // the symbol loop counts a chunk's samples in 32-bit integers; a longer
+    // call is split into chunks of max_samples_per_call (a C# span holds at
+    // most 2^31 - 1 floats anyway)
+    if (p->max_samples_per_call > kMaxSamplesPerCall)
+        return fail(QPSK_ERR_OUT_OF_RANGE, "max_samples_per_call above 2^30");
     auto *h = new qpsk_demod();
     h->p = *p;
     h->S = n_streams;
@@ -459,8 +513,11 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
         return cleanup_fail(rc);
     if (p->enable_fll && (rc = dev_alloc(&h->d_fll_out[0], static_cast<size_t>(2 * S * h->n_max))))
         return cleanup_fail(rc);
-    if (hipHostMalloc(reinterpret_cast<void **>(&h->h_counts), 2 * S * sizeof(int64_t)) != hipSuccess)
+    if (hipHostMalloc(reinterpret_cast<void **>(&h->h_counts), 2 * S * sizeof(int64_t)) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&h->h_flags), sizeof(uint32_t)) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipHostMalloc"));
+    if ((rc = dev_alloc(&h->d_flags, 2)) || hipMemset(h->d_flags, 0, 2 * sizeof(uint32_t)) != hipSuccess)
+        return cleanup_fail(rc ? rc : fail(QPSK_ERR_DEVICE, "hipMemset"));
     std::vector<float> hrev(h->T);
     for (int k = 0; k < h->T; ++k) hrev[k] = h->d.rrc_f32[h->T - 1 - k];
     // Fresh instances: zero delay lines (FIRFilter.cs:50-51), M&M baseIndex = 1
@@ -503,6 +560,11 @@ int qpsk_demod_destroy(qpsk_demod *h) {
     hipFree(h->d_syms);
     hipFree(h->d_counts);
     if (h->h_counts) hipHostFree(h->h_counts);
+    if (h->h_flags) hipHostFree(h->h_flags);
+    hipFree(h->d_flags);
+    hipFree(h->d_acc);
+    hipFree(h->d_xbits);
+    hipFree(h->d_xsyms);
     for (auto &set : h->ev_pool)
         for (auto &e : set) hipEventDestroy(e);
     if (h->e_in) hipEventDestroy(h->e_in);
@@ -553,14 +615,17 @@ int qpsk_demod_stage_times(const qpsk_demod *h, float *ms, int32_t n) {
     return k;
 }
 
-int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t stride_floats,
-                       int64_t n_samples, const int64_t *lengths, int32_t mem, uint8_t *bits,
-                       int64_t bits_stride_bytes, int64_t *n_bits, float *syms,
-                       int64_t syms_stride_floats, int64_t *n_syms) {
-    Call c{mode, iq, stride_floats, n_samples, lengths, mem, bits, bits_stride_bytes, n_bits,
-           syms, syms_stride_floats, n_syms};
+}  // extern "C"
+
+namespace {
+
+// One validated call of at most max_samples_per_call samples per stream.
+int process_one(qpsk_demod *h, const Call &c) {
     int rc;
-    if ((rc = validate(h, c))) return rc;
+    const int32_t mem = c.mem;
+    const float *iq = c.iq;
+    const int64_t stride_floats = c.stride_floats;
+    const int64_t *lengths = c.lengths;
     const int S = h->S;
     const int64_t n_call = c.n_call;
     hipStream_t st = h->stream;
@@ -570,6 +635,7 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
     hipEvent_t *ev = next_events(h, &rc);
     if (rc) return rc;
     EV(0, st);
+    if (mem == QPSK_MEM_HOST && !c.append) HIP_TRY(hipMemsetAsync(h->d_flags + 1, 0, sizeof(uint32_t), st));
 
     // ---- input -----------------------------------------------------------
     const float *x = iq;
@@ -597,14 +663,11 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
     return run_loop(h, c, d_len, h->d_mf[0], st, ev);
 }
 
-int qpsk_demod_process_async(qpsk_demod *h, int32_t mode, const float *iq, int64_t stride_floats,
-                             int64_t n_samples, const int64_t *lengths, uint8_t *bits,
-                             int64_t bits_stride_bytes, int64_t *n_bits, float *syms,
-                             int64_t syms_stride_floats, int64_t *n_syms) {
-    Call c{mode, iq, stride_floats, n_samples, lengths, QPSK_MEM_DEVICE, bits, bits_stride_bytes,
-           n_bits, syms, syms_stride_floats, n_syms};
+int process_async_one(qpsk_demod *h, const Call &c) {
     int rc;
-    if ((rc = validate(h, c))) return rc;
+    const float *iq = c.iq;
+    const int64_t stride_floats = c.stride_floats;
+    const int64_t *lengths = c.lengths;
     HIP_TRY(hipSetDevice(h->p.device));
     if ((rc = pipe_setup(h))) return rc;
     const int S = h->S;
@@ -657,6 +720,169 @@ int qpsk_demod_process_async(qpsk_demod *h, int32_t mode, const float *iq, int64
     HIP_TRY(hipEventRecord(h->e_back[b], B));
     h->back_rec[b] = true;
     h->last_back = b;
+    return QPSK_OK;
+}
+
+// QPSK_STATUS_* raised by the host-memory call that just finished -> status
+int host_call_status(qpsk_demod *h) {
+    const uint32_t f = *h->h_flags;
+    if (f & QPSK_STATUS_CARRY_OVERFLOW)
+        return fail(QPSK_ERR_STATE, "symbol-sync queue over 64 retained samples (sps > 60?)");
+    if (f & QPSK_STATUS_OUTPUT_TRUNCATED) return fail(QPSK_ERR_CAPACITY, "output row truncated");
+    if (f & QPSK_STATUS_NONFINITE_TIMING)
+        return fail(QPSK_ERR_STATE, "non-finite sample reached the symbol timing loop");
+    return QPSK_OK;
+}
+
+// A call longer than max_samples_per_call (QPSKDeModulator.cs:345-360 accepts
+// any span): consecutive internal chunks of at most n_max samples per stream,
+// each chunk's rows appended behind the previous one's, so the caller sees the
+// output of one call (the chain carries its state across chunks exactly as
+// across calls).  Host-memory outputs are staged in device rows of the whole
+// call and copied back once.
+int process_chunked(qpsk_demod *h, const Call &c, bool async) {
+    const int S = h->S;
+    const int64_t N = h->n_max;
+    int rc;
+    HIP_TRY(hipSetDevice(h->p.device));
+    if (!h->d_acc && (rc = dev_alloc(&h->d_acc, 2 * static_cast<size_t>(S)))) return rc;
+    if (c.syms && !h->d_syms && (rc = dev_alloc(&h->d_syms, static_cast<size_t>(2 * S * h->syms_cap))))
+        return rc;
+    const bool host = c.mem == QPSK_MEM_HOST;
+    const int64_t bytes_row = (2 * c.max_sym + 7) / 8;
+    uint8_t *dbits = c.bits;
+    int64_t dbits_stride = c.bits_stride_bytes;
+    float *dsyms = c.syms;
+    int64_t dsyms_stride = c.syms_stride_floats;
+    if (host) {
+        if (async) return fail(QPSK_ERR_ARGUMENT, "pipelined calls take device memory");
+        if (c.bits) {
+            const size_t need = static_cast<size_t>(S) * bytes_row;
+            if (need > h->xbits_bytes) {
+                hipFree(h->d_xbits);
+                h->d_xbits = nullptr;
+                h->xbits_bytes = 0;
+                if ((rc = dev_alloc(&h->d_xbits, need))) return rc;
+                h->xbits_bytes = need;
+            }
+            dbits = h->d_xbits;
+            dbits_stride = bytes_row;
+        }
+        if (c.syms) {
+            const size_t need = static_cast<size_t>(S) * 2 * c.max_sym * sizeof(float);
+            if (need > h->xsyms_bytes) {
+                hipFree(h->d_xsyms);
+                h->d_xsyms = nullptr;
+                h->xsyms_bytes = 0;
+                if ((rc = dev_alloc(&h->d_xsyms, need / sizeof(float)))) return rc;
+                h->xsyms_bytes = need;
+            }
+            dsyms = h->d_xsyms;
+            dsyms_stride = 2 * c.max_sym;
+        }
+        HIP_TRY(hipMemsetAsync(h->d_flags + 1, 0, sizeof(uint32_t), h->stream));
+    }
+    const int64_t K = (c.n_call + N - 1) / N;
+    std::vector<int64_t> len_k(c.lengths ? S : 0);
+    for (int64_t k = 0; k < K; ++k) {
+        const int64_t off = k * N;
+        Call sub = c;
+        sub.iq = c.iq + 2 * off;
+        if (c.lengths) {
+            int64_t m = 0;
+            for (int s = 0; s < S; ++s) {
+                len_k[s] = std::min(N, std::max<int64_t>(0, c.lengths[s] - off));
+                m = std::max(m, len_k[s]);
+            }
+            sub.lengths = len_k.data();
+            sub.n_samples = 0;
+            sub.n_call = m;
+        } else {
+            sub.n_samples = std::min(N, c.n_samples - off);
+            sub.n_call = sub.n_samples;
+        }
+        sub.max_sym = qpsk_demod_max_symbols(h, sub.n_call);
+        sub.append = true;
+        sub.first = k == 0;
+        sub.last = k == K - 1;
+        sub.dst_bits = dbits;
+        sub.dst_bits_stride = dbits_stride;
+        sub.dst_syms = dsyms;
+        sub.dst_syms_stride = dsyms_stride;
+        sub.dst_n_bits = host ? nullptr : c.n_bits;
+        sub.dst_n_syms = host ? nullptr : c.n_syms;
+        if ((rc = async ? process_async_one(h, sub) : process_one(h, sub))) return rc;
+    }
+    if (!host) return QPSK_OK;
+    hipStream_t st = h->stream;
+    if (c.bits && bytes_row > 0)
+        HIP_TRY(hipMemcpy2DAsync(c.bits, c.bits_stride_bytes, dbits, dbits_stride, bytes_row, S,
+                                 hipMemcpyDeviceToHost, st));
+    if (c.syms && c.max_sym > 0)
+        HIP_TRY(hipMemcpy2DAsync(c.syms, c.syms_stride_floats * sizeof(float), dsyms,
+                                 dsyms_stride * sizeof(float), 2 * c.max_sym * sizeof(float), S,
+                                 hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(h->h_counts, h->d_acc, 2 * S * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(h->h_flags, h->d_flags + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (c.n_bits) std::memcpy(c.n_bits, h->h_counts, S * sizeof(int64_t));
+    if (c.n_syms) std::memcpy(c.n_syms, h->h_counts + S, S * sizeof(int64_t));
+    h->status_host |= *h->h_flags;
+    return host_call_status(h);
+}
+
+}  // namespace (calls)
+
+extern "C" {
+
+int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t stride_floats,
+                       int64_t n_samples, const int64_t *lengths, int32_t mem, uint8_t *bits,
+                       int64_t bits_stride_bytes, int64_t *n_bits, float *syms,
+                       int64_t syms_stride_floats, int64_t *n_syms) {
+    Call c{mode, iq, stride_floats, n_samples, lengths, mem, bits, bits_stride_bytes, n_bits,
+           syms, syms_stride_floats, n_syms};
+    int rc;
+    if ((rc = validate(h, c))) return rc;
+    if (c.n_call > h->n_max) return process_chunked(h, c, false);
+    if ((rc = process_one(h, c))) return rc;
+    return c.mem == QPSK_MEM_HOST ? host_call_status(h) : QPSK_OK;
+}
+
+int qpsk_demod_process_async(qpsk_demod *h, int32_t mode, const float *iq, int64_t stride_floats,
+                             int64_t n_samples, const int64_t *lengths, uint8_t *bits,
+                             int64_t bits_stride_bytes, int64_t *n_bits, float *syms,
+                             int64_t syms_stride_floats, int64_t *n_syms) {
+    Call c{mode, iq, stride_floats, n_samples, lengths, QPSK_MEM_DEVICE, bits, bits_stride_bytes,
+           n_bits, syms, syms_stride_floats, n_syms};
+    int rc;
+    if ((rc = validate(h, c))) return rc;
+    if (c.n_call > h->n_max) return process_chunked(h, c, true);
+    return process_async_one(h, c);
+}
+
+int qpsk_demod_last_mf(qpsk_demod *h, float *out, int64_t stride_floats, int64_t n_samples, int32_t mem) {
+    if (!h || !out) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    if (n_samples < 0 || n_samples > h->n_max || stride_floats < 2 * n_samples)
+        return fail(QPSK_ERR_ARGUMENT, "n_samples / stride_floats out of range");
+    if (mem != QPSK_MEM_HOST && mem != QPSK_MEM_DEVICE) return fail(QPSK_ERR_ARGUMENT, "unknown mem");
+    HIP_TRY(hipSetDevice(h->p.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (n_samples == 0) return QPSK_OK;
+    HIP_TRY(hipMemcpy2D(out, stride_floats * sizeof(float), h->d_mf[0] + 2 * kMfPrefix,
+                        2 * h->mf_stride * sizeof(float), 2 * n_samples * sizeof(float), h->S,
+                        mem == QPSK_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice));
+    return QPSK_OK;
+}
+
+int qpsk_demod_status(qpsk_demod *h, uint32_t *flags) {
+    if (!h || !flags) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    int rc;
+    if ((rc = drain_async(h))) return rc;
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipMemcpy(h->h_flags, h->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(h->d_flags, 0, sizeof(uint32_t)));
+    *flags = *h->h_flags | h->status_host;
+    h->status_host = 0;
     return QPSK_OK;
 }
 

@@ -172,7 +172,7 @@ int qpsk_rx_submit(qpsk_rx *r, const float *iq, int64_t stride_floats, int64_t n
     } else if (n_samples < 0) {
         return fail(QPSK_ERR_ARGUMENT, "negative n_samples");
     }
-    if (n_call > r->n_max) return fail(QPSK_ERR_CAPACITY, "call longer than max_samples_per_call");
+    if (n_call > r->n_max) return fail(QPSK_ERR_ARGUMENT, "chunk longer than the ring slots (max_samples_per_call)");
     if (n_call > 0 && !iq) return fail(QPSK_ERR_ARGUMENT_NULL, "SamplesIQ is null");
     if (n_call > 0 && stride_floats < 2 * n_call) return fail(QPSK_ERR_ARGUMENT, "stride too small");
     RX_TRY(hipSetDevice(r->device));

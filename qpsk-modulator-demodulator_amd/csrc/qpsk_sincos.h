@@ -1,7 +1,7 @@
 /*
  * qpsk_sincos.h -- PRODUCT copy of the portable double/float sin+cos used as the
  * deterministic stand-in for .NET Math.Cos/Math.Sin (CostasLoopQpsk.cs:69-70)
- * and MathF.Cos/MathF.Sin (Band-Edge Filter.cs:108-109).
+ * (the float MathF.Cos/MathF.Sin of the FLL are glibc's, qpsk_sincosf.h).
  *
  * Host + device.  The oracle keeps its own copy (oracle/or_sincos.h); a CPU
  * test sweeps both and requires bitwise-identical results, and the GPU parity
@@ -21,6 +21,7 @@
 #define QPSK_SINCOS_H
 #include <math.h>
 #include "qpsk_sincos_table.h"
+#include "qpsk_sincosf.h"
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define QPSK_HD __host__ __device__
@@ -93,31 +94,6 @@ QPSK_HD static inline void qpsk_sincos_tab_core_k(double x, const double *tab, c
     *c = tc + fma(-ts, r, fma(-ts, r3p, fma(tc, cm, lc)));
 }
 
-/* The same core for a FLOAT argument |x| <= 2pi (the FLL phase after its
- * wrap), two f64 ops shorter: kb from one fma and no k*P3 term.  For every such
- * float it returns the same doubles as qpsk_sincos_tab_core_k, checked
- * exhaustively over all 2.17e9 of them (tools/check_sincosf_core.c; a strided
- * subset runs in tests/test_oracle.py).  Why: x - k*P1 is exact for a float x,
- * |r| stays far above 2^-60, so k*P3 (< 2^-106) is below half an ulp of r, and
- * the fused x*INV + SH rounds to the same integer k. */
-QPSK_HD static inline void qpsk_sincos_tab_core_f(double x, const double *tab, const double *lo,
-                                             const qpsk_sincos_consts *K, double *s, double *c)
-{
-    union { double d; unsigned long long u; } kb;
-    kb.d = fma(x, K->INV, K->SH);
-    const double k = kb.d - K->SH;
-    double r = fma(-k, K->P1, x);
-    r = fma(-k, K->P2, r);
-    const unsigned i = (unsigned)(kb.u & 511u) * 2u;
-    const double ts = tab[i], tc = tab[i + 1];
-    const double ls = lo[i], lc = lo[i + 1];
-    const double z = r * r;
-    const double r3p = (r * z) * fma(z, K->S5, K->S3);
-    const double cm = z * fma(z, fma(z, K->C6, K->C4), -0.5);
-    *s = ts + fma(tc, r, fma(tc, r3p, fma(ts, cm, ls)));
-    *c = tc + fma(-ts, r, fma(-ts, r3p, fma(tc, cm, lc)));
-}
-
 /* sin and cos of x, |x| <= 2^40 or NaN, given the 512-entry table (any address
  * space: the GPU kernels pass a copy staged in LDS).  Straight-line: the GPU
  * Costas loop is issue-bound and every instruction costs issue slots.  NaN
@@ -142,17 +118,10 @@ static inline void qpsk_sincos(double x, double *s, double *c)
     qpsk_sincos_tab(x, qpsk_sincos_table_host, qpsk_sincos_table_host_lo, s, c);
 }
 
-QPSK_HD static inline void qpsk_sincosf_tab(float x, const double *tab, const double *lo, float *s,
-                                       float *c)
-{
-    double sd, cd;
-    qpsk_sincos_tab((double)x, tab, lo, &sd, &cd);
-    *s = (float)sd;
-    *c = (float)cd;
-}
-
+/* float sin/cos (MathF.Sin/Cos of the FLL phase): glibc's sinf/cosf restated,
+ * qpsk_sincosf.h */
 static inline void qpsk_sincosf(float x, float *s, float *c)
 {
-    qpsk_sincosf_tab(x, qpsk_sincos_table_host, qpsk_sincos_table_host_lo, s, c);
+    qpsk_sincosf_glibc(x, s, c);
 }
 #endif

@@ -49,6 +49,7 @@ struct SynthArgs {
     double cfo_hz, lo_ppm, lo_hz, fs;
     double noise_sigma;   // per component, 0 = none
     int differential;
+    int carrier;          // 0: lo_ppm = cfo_hz = 0, the modulator's own baseband
     uint8_t *quad;        // [S][nsym] quadrant / symbol index
     uint8_t *bits;        // [S][bits_stride] payload bits MSB-first
     int64_t bits_stride;
@@ -123,10 +124,13 @@ __global__ void synth_samples_kernel(SynthArgs a, Pulse p) {
     if (a.cfo_hz > 0.0) f = (2.0 * u1 - 1.0) * a.cfo_hz;
     else if (a.lo_ppm > 0.0) f = a.lo_hz * ((2.0 * u1 - 1.0) - (2.0 * u2 - 1.0)) * a.lo_ppm * 1e-6;
     const double ph = 2.0 * 3.14159265358979323846 * (u3 + f * static_cast<double>(i) / a.fs);
-    double sn, cs;
-    sincos(ph, &sn, &cs);
-    double zr = yr * cs - yi * sn;
-    double zi = yr * sn + yi * cs;
+    double zr = yr, zi = yi;
+    if (a.carrier) {
+        double sn, cs;
+        sincos(ph, &sn, &cs);
+        zr = yr * cs - yi * sn;
+        zi = yr * sn + yi * cs;
+    }
     if (a.noise_sigma > 0.0) {
         uint64_t h = a.seed ^ (gs << 40) ^ static_cast<uint64_t>(i) ^ 0xA5A5A5A5ULL;
         const double n1 = 1.0 - u01(splitmix64(h));
@@ -206,6 +210,7 @@ int qpsk_synth_generate(const qpsk_synth_params *p, int32_t device, void *hip_st
     // Es = 1 per symbol (unit-energy RRC, |sym| = 1): per-sample complex N0 = 1/EsN0
     a.noise_sigma = p->esn0_db < 200.0 ? std::sqrt(0.5 * std::pow(10.0, -p->esn0_db / 10.0)) : 0.0;
     a.differential = p->differential;
+    a.carrier = (p->lo_ppm > 0.0 || p->cfo_hz > 0.0) ? 1 : 0;
     a.bits = tx_bits_dev;
     a.bits_stride = bits_stride_bytes;
     a.iq = iq_dev;

@@ -33,6 +33,9 @@ QPSK_ERR_OUT_OF_RANGE = -3
 QPSK_ERR_DEVICE = -4
 QPSK_ERR_CAPACITY = -5
 QPSK_ERR_STATE = -6
+STATUS_CARRY_OVERFLOW = 1
+STATUS_OUTPUT_TRUNCATED = 2
+STATUS_NONFINITE_TIMING = 4
 MEM_HOST = 0
 MEM_DEVICE = 1
 MODE_DEMODULATE = 0
@@ -77,6 +80,18 @@ class SynthParams(C.Structure):
         ("esn0_db", C.c_double),
         ("first_stream", C.c_int64),
         ("reserved", C.c_int32 * 6),
+    ]
+
+
+class ModParams(C.Structure):
+    _fields_ = [
+        ("sample_rate", C.c_int32),
+        ("symbol_rate", C.c_int32),
+        ("rrc_alpha", C.c_double),
+        ("rrc_span", C.c_int32),
+        ("differential", C.c_int32),
+        ("device", C.c_int32),
+        ("reserved", C.c_int32 * 7),
     ]
 
 
@@ -130,6 +145,19 @@ def lib():
                                            _i64p, C.c_void_p, C.c_int64, C.c_void_p,
                                            C.c_void_p, C.c_int64, C.c_void_p]
     L.qpsk_demod_pipeline_wait.argtypes = [C.c_void_p, C.c_void_p]
+    L.qpsk_demod_status.argtypes = [C.c_void_p, C.POINTER(C.c_uint32)]
+    L.qpsk_demod_last_mf.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int32]
+    L.qpsk_mod_params_init.argtypes = [C.POINTER(ModParams), C.c_int32, C.c_int32]
+    L.qpsk_mod_create.argtypes = [C.POINTER(ModParams), C.c_char_p, C.POINTER(C.c_void_p)]
+    L.qpsk_mod_destroy.argtypes = [C.c_void_p]
+    L.qpsk_mod_set_stream.argtypes = [C.c_void_p, C.c_void_p]
+    L.qpsk_mod_output_floats.argtypes = [C.c_void_p, C.c_int64, C.c_int32]
+    L.qpsk_mod_output_floats.restype = C.c_int64
+    L.qpsk_mod_modulate.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p, C.c_int32,
+                                    C.c_int32, C.c_void_p, C.c_int64, C.c_void_p]
+    L.qpsk_mod_modulate_bytes.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p,
+                                          C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
+                                          C.c_void_p, C.c_int64, C.c_void_p]
     L.qpsk_demod_pipeline_depth.argtypes = [C.c_void_p]
     L.qpsk_demod_max_symbols.argtypes = [C.c_void_p, C.c_int64]
     L.qpsk_demod_max_symbols.restype = C.c_int64
@@ -185,7 +213,9 @@ EXPORTED_SYMBOLS = [
     "qpsk_framer_dev_push", "qpsk_framer_dev_status", "qpsk_tsc_find_device",
     "qpsk_synth_params_init", "qpsk_synth_generate", "qpsk_demod_process_async",
     "qpsk_demod_pipeline_wait", "qpsk_demod_pipeline_depth", "qpsk_rx_create", "qpsk_rx_destroy",
-    "qpsk_rx_next_slot", "qpsk_rx_submit", "qpsk_rx_collect",
+    "qpsk_rx_next_slot", "qpsk_rx_submit", "qpsk_rx_collect", "qpsk_demod_status", "qpsk_demod_last_mf",
+    "qpsk_mod_params_init", "qpsk_mod_create", "qpsk_mod_destroy", "qpsk_mod_set_stream",
+    "qpsk_mod_output_floats", "qpsk_mod_modulate", "qpsk_mod_modulate_bytes",
 ]
 
 _EXC = {
@@ -288,6 +318,19 @@ class BatchDemodulator:
         _check(lib().qpsk_demod_fll_taps(self._h, lo.ctypes.data_as(_f32p), up.ctypes.data_as(_f32p), 80))
         return lo, up
 
+    def status(self) -> int:
+        """OR of the STATUS_* flags raised since the last status() call (waits
+        for every queued call; qpsk_demod_status)."""
+        f = C.c_uint32()
+        _check(lib().qpsk_demod_status(self._h, C.byref(f)))
+        return int(f.value)
+
+    def last_mf(self, n: int) -> np.ndarray:
+        """[S, 2n] float32: the matched-filter output of the last synchronous call."""
+        out = np.zeros((self.S, max(2 * int(n), 2)), dtype=np.float32)
+        _check(lib().qpsk_demod_last_mf(self._h, out.ctypes.data, out.shape[1], int(n), MEM_HOST))
+        return out[:, : 2 * int(n)]
+
     def get_state(self) -> bytes:
         n = lib().qpsk_demod_state_bytes(self._h)
         buf = C.create_string_buffer(n)
@@ -310,7 +353,11 @@ class BatchDemodulator:
         n = iq.shape[1] // 2
         if lengths is not None:
             lengths = np.ascontiguousarray(lengths, dtype=np.int64)
+            if lengths.shape != (self.S,):
+                raise ValueError("lengths must hold one count per stream")
             nmax = int(lengths.max()) if lengths.size else 0
+            if nmax > n:
+                raise ValueError("a length exceeds the row (iq.shape[1] // 2 samples)")
         else:
             nmax = n
         ms = max(self.max_symbols(nmax), 1)
@@ -320,7 +367,7 @@ class BatchDemodulator:
         n_syms = np.zeros(self.S, dtype=np.int64)
         syms = np.zeros((self.S, 2 * ms), dtype=np.float32) if (want_syms or mode == MODE_CONSTELLATION) else None
         _check(lib().qpsk_demod_process(
-            self._h, int(mode), iq.ctypes.data if iq.size else None, max(iq.shape[1], 2 * nmax), n,
+            self._h, int(mode), iq.ctypes.data if iq.size else None, iq.shape[1], n,
             lengths.ctypes.data_as(_i64p) if lengths is not None else None, MEM_HOST,
             bits.ctypes.data if mode == MODE_DEMODULATE else None, bstride,
             n_bits.ctypes.data if mode == MODE_DEMODULATE else None,
@@ -329,11 +376,25 @@ class BatchDemodulator:
         return bits, n_bits, syms, n_syms
 
     # ---- device path (torch tensors resident in HBM) ---------------------
+    def _check_device_args(self, iq_dev, n, bits_dev, n_bits_dev, syms_dev, n_syms_dev):
+        import torch
+        if iq_dev.dtype != torch.float32 or iq_dev.dim() != 2 or iq_dev.shape[0] != self.S:
+            raise ValueError("iq_dev must be a float32 [n_streams, >= 2n] tensor")
+        if iq_dev.stride(1) != 1 or iq_dev.shape[1] < 2 * int(n):
+            raise ValueError("iq_dev rows must be contiguous and hold 2n floats")
+        for t, dt, what in ((bits_dev, torch.uint8, "bits_dev"), (syms_dev, torch.float32, "syms_dev")):
+            if t is not None and (t.dtype != dt or t.dim() != 2 or t.shape[0] != self.S or t.stride(1) != 1):
+                raise ValueError(f"{what} must be a contiguous-row {dt} [n_streams, k] tensor")
+        for t, what in ((n_bits_dev, "n_bits_dev"), (n_syms_dev, "n_syms_dev")):
+            if t is not None and (t.dtype != torch.int64 or t.numel() != self.S or not t.is_contiguous()):
+                raise ValueError(f"{what} must be a contiguous int64 [n_streams] tensor")
+
     def process_device(self, iq_dev, n, bits_dev, n_bits_dev, mode=MODE_DEMODULATE,
                        syms_dev=None, n_syms_dev=None):
         """All arguments are torch CUDA tensors; stream-ordered on the handle's
         stream (bind torch's stream with set_stream first)."""
-        bstride = bits_dev.stride(0) * bits_dev.element_size()
+        self._check_device_args(iq_dev, n, bits_dev, n_bits_dev, syms_dev, n_syms_dev)
+        bstride = bits_dev.stride(0) * bits_dev.element_size() if bits_dev is not None else 0
         sstride = syms_dev.stride(0) if syms_dev is not None else 0
         _check(lib().qpsk_demod_process(
             self._h, int(mode), iq_dev.data_ptr(), iq_dev.stride(0), int(n), None, MEM_DEVICE,
@@ -347,6 +408,7 @@ class BatchDemodulator:
         """Pipelined call (qpsk_demod_process_async): returns once queued; the
         outputs are complete after pipeline_wait().  lengths: optional host
         int64 array of per-stream sample counts."""
+        self._check_device_args(iq_dev, n, bits_dev, n_bits_dev, syms_dev, n_syms_dev)
         bstride = bits_dev.stride(0) * bits_dev.element_size() if bits_dev is not None else 0
         sstride = syms_dev.stride(0) if syms_dev is not None else 0
         if lengths is not None:
@@ -620,6 +682,91 @@ class QPSKDeModulator:
     def DeModulateTextUtf8(self, samples, startMarker="\u0002", endMarker="\u0003") -> str:
         p = self.DeModulateBytes(samples, startMarker.encode("utf-8"), endMarker.encode("utf-8"))
         return p.decode("utf-8", errors="replace") if p else ""
+
+
+class QPSKModulator:
+    """The reference's QPSKModulator (QPSKModulator.cs:18-167) on the GPU:
+    Modulate / ModulateBytes / ModulateTextUtf8 for one stream, and the
+    batched form (modulate_batch) that one call runs over many bit strings."""
+
+    def __init__(self, SampleRate, SymbolRate, RrcAlpha=0.9, rrcSpan=6, differentialEncoding=True,
+                 tsc=None, device=0):
+        p = ModParams()
+        lib().qpsk_mod_params_init(C.byref(p), int(SampleRate), int(SymbolRate))
+        p.rrc_alpha = float(RrcAlpha)
+        p.rrc_span = int(rrcSpan)
+        p.differential = 1 if differentialEncoding else 0
+        p.device = int(device)
+        h = C.c_void_p()
+        _check(lib().qpsk_mod_create(C.byref(p), tsc.encode() if tsc else None, C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().qpsk_mod_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def output_floats(self, n_bits, pulse_shaping=True) -> int:
+        return int(lib().qpsk_mod_output_floats(self._h, int(n_bits), 1 if pulse_shaping else 0))
+
+    def modulate_batch(self, bit_rows, n_bits, pulse_shaping=True):
+        """bit_rows [S, B] uint8 packed MSB-first, n_bits [S] -> list of float32 arrays."""
+        rows = np.ascontiguousarray(bit_rows, dtype=np.uint8)
+        nb = np.ascontiguousarray(n_bits, dtype=np.int64)
+        S = nb.size
+        if rows.ndim != 2 or rows.shape[0] != S:
+            raise ValueError("bit_rows must be [S, B] with one n_bits per row")
+        if S and int(nb.max()) > 8 * rows.shape[1]:
+            raise ValueError("a bit count exceeds its row")
+        width = max(self.output_floats(int(nb.max()) if S else 0, pulse_shaping), 2)
+        out = np.zeros((S, width), dtype=np.float32)
+        nout = np.zeros(S, dtype=np.int64)
+        _check(lib().qpsk_mod_modulate(self._h, S, rows.ctypes.data if rows.size else None,
+                                       rows.shape[1], nb.ctypes.data, 1 if pulse_shaping else 0,
+                                       MEM_HOST, out.ctypes.data, width, nout.ctypes.data))
+        return [out[s, : int(nout[s])].copy() for s in range(S)]
+
+    def Modulate(self, data: str, pulseShaping=True) -> np.ndarray:
+        if data is None:
+            raise ValueError("data")                                   # ArgumentNullException :107
+        if any(c not in "01" for c in data):
+            raise ValueError("data must be a '0'/'1' string")
+        row = pack_bits(data) if data else np.zeros(1, np.uint8)
+        return self.modulate_batch(row[None, :], [len(data)], pulseShaping)[0]
+
+    def ModulateBytes(self, payload: bytes, startMarker: bytes, endMarker: bytes,
+                      pulseShaping=True) -> np.ndarray:
+        if len(startMarker) == 0:
+            raise ValueError("startMarker cannot be empty.")              # :60
+        if len(endMarker) == 0:
+            raise ValueError("endMarker cannot be empty.")                # :61
+        pay = np.frombuffer(bytes(payload), dtype=np.uint8).copy()
+        st = np.frombuffer(bytes(startMarker), dtype=np.uint8).copy()
+        en = np.frombuffer(bytes(endMarker), dtype=np.uint8).copy()
+        nbits = 8 * (st.size + pay.size + en.size)
+        width = max(self.output_floats(nbits, pulseShaping), 2)
+        out = np.zeros((1, width), dtype=np.float32)
+        nout = np.zeros(1, dtype=np.int64)
+        npay = np.array([pay.size], dtype=np.int64)
+        _check(lib().qpsk_mod_modulate_bytes(self._h, 1, pay.ctypes.data if pay.size else None,
+                                             max(pay.size, 1), npay.ctypes.data, st.ctypes.data,
+                                             st.size, en.ctypes.data, en.size,
+                                             1 if pulseShaping else 0, out.ctypes.data, width,
+                                             nout.ctypes.data))
+        return out[0, : int(nout[0])].copy()
+
+    def ModulateTextUtf8(self, text: str, startMarker="\u0002", endMarker="\u0003",
+                         pulseShaping=True) -> np.ndarray:
+        if text is None:
+            raise ValueError("text")                                   # :81
+        return self.ModulateBytes(text.encode("utf-8"), startMarker.encode("utf-8"),
+                                  endMarker.encode("utf-8"), pulseShaping)
 
 
 def synth_generate(n_streams, n_samples, sample_rate, symbol_rate, rrc_alpha=float(np.float32(0.4)),

@@ -374,8 +374,9 @@ class FLL:
         out = np.zeros_like(x)
         two_pi = F(2) * PI_F
         for t in range(x.shape[0]):
-            s, c = portable_sincos(float(self.phase))
-            s, c = F(s), F(c)
+            # MathF.Sin / MathF.Cos (Band-Edge Filter.cs:108-109): the C runtime's
+            c = F(_libm.cosf(float(self.phase)))
+            s = F(_libm.sinf(float(self.phase)))
             xi, xq = x[t, 0], x[t, 1]
             oi = xi * c - xq * s
             oq = xi * s + xq * c

@@ -20,6 +20,7 @@ import common as K
 import oracle as O
 
 TOTAL = 6
+K_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -95,3 +96,79 @@ def test_ber_windowed_realignment_counts_slips_not_errors():
     assert slips == 1
     assert e <= 5 and e >= 5 - lost    # an error inside a key loses that window instead
     assert tot > 25000
+
+
+# ---- the RCCL scatter/gather leg through the same code, gloo ----
+SG_STREAMS = 3          # per rank
+SG_BITS = 600
+
+
+def _sg_synth(first, count):
+    """Global stream ids -> rows, as Q.synth_generate does on the GPU."""
+    sigs = [K.stream_signal(4000 + g, sps=8, span=8, n_bits=SG_BITS) for g in range(first, first + count)]
+    n = min(x.size for x in sigs)
+    return torch.from_numpy(np.stack([x[:n] for x in sigs]))
+
+
+def _sg_demod(x):
+    bits, nb, _, _ = O.demod_batch_packed(x.numpy(), K.FS, K.FS // 8, n_threads=1,
+                                          rrc_alpha=K.ALPHA, rrc_span=8, trig=O.TRIG_PORTABLE)
+    return torch.from_numpy(bits), torch.from_numpy(nb)
+
+
+def _sg_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = _sg_synth(0, 1).shape[1] // 2
+        rec, gathered = bench.split_gather(_sg_synth, _sg_demod, SG_STREAMS, n, world, rank,
+                                           torch.device("cpu"), host_collectives=True)
+        if rank == 0:
+            q.put((rec, gathered[0].numpy(), gathered[1].numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_split_gather_matches_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sg_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        rec, bits, nb = q.get(timeout=180)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert rec["shards_match_local_synth"] is True
+    assert rec["scatter_ms"] >= 0 and rec["gather_ms"] >= 0
+    # the gathered rows equal one process demodulating the whole batch
+    rb, rnb = _sg_demod(_sg_synth(0, 2 * SG_STREAMS))
+    assert np.array_equal(nb, rnb.numpy())
+    bad, _ = bench.compare_rows(bits, nb, rb.numpy(), rnb.numpy())
+    assert bad == []
+
+
+def test_compare_rows_masks_the_partial_byte():
+    ref = np.array([[0b10110000, 0xFF]], np.uint8)
+    got = np.array([[0b10111111, 0x00]], np.uint8)
+    assert bench.compare_rows(got, [4], ref, [4])[0] == []
+    assert bench.compare_rows(got, [5], ref, [5])[0] == [0]
+    assert bench.compare_rows(got, [4], ref, [6])[0] == [0]
+
+
+def test_pick_streams_covers_the_batch_tail():
+    assert bench.pick_streams(100, 500) == list(range(100))
+    idx = bench.pick_streams(4096, 200)
+    assert idx[:3] == [0, 1, 2] and idx[-64:] == list(range(4032, 4096)) and len(idx) == 200
+
+
+def test_bench_gpus_flag_must_match_world_size():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(K_ROOT, "bench.py"), "--gpus", "2"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in (r.stderr + r.stdout)

@@ -147,15 +147,18 @@ def test_fll_ctor_validation():
         O.OracleDemod(K.FS, K.FS // 8, 0.4, 8, cfo_loop_bw=-1.0)
 
 
-def test_float_argument_sincos_core_equals_full_core(tmp_path):
-    """qpsk_sincos_tab_core_f (FLL fast path) == qpsk_sincos_tab_core for float
-    |x| <= 2pi.  Every 61st float here; tools/check_sincosf_core.c with stride 1
-    covers all 2.17e9 (FLL)."""
+def test_fll_float_trig_equals_glibc(tmp_path):
+    """MathF.Sin/Cos (Band-Edge Filter.cs:108-109) are glibc's sinf/cosf on a
+    Linux host.  The oracle's restatement (or_sinf/or_cosf) and the product's
+    fused forms (qpsk_sincosf_glibc, _small, _fast) must equal the real glibc
+    bit for bit: every 3rd float here (1.4e9 inputs, a few seconds);
+    tools/check_glibc_sincosf.c with stride 1 covers all 2^32."""
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    exe = str(tmp_path / "check_sincosf")
-    subprocess.check_call(["gcc", "-O2", "-fopenmp", "-ffp-contract=off",
+    exe = str(tmp_path / "check_glibc_sincosf")
+    subprocess.check_call(["gcc", "-O2", "-fopenmp", "-ffp-contract=off", "-mfma",
+                           "-I" + os.path.join(root, "oracle"),
                            "-I" + os.path.join(root, "qpsk-modulator-demodulator_amd", "csrc"),
-                           "-o", exe, os.path.join(root, "tools", "check_sincosf_core.c"), "-lm"])
-    out = subprocess.run([exe, "61"], capture_output=True, text=True, check=True).stdout
+                           "-o", exe, os.path.join(root, "tools", "check_glibc_sincosf.c"), "-lm"])
+    out = subprocess.run([exe, "3"], capture_output=True, text=True).stdout
     assert out.strip().endswith(" 0 differ"), out
