@@ -45,6 +45,7 @@ struct LoopArgs {
     int S;
     unsigned long long *probe;   // diagnostic cycle stamps (QPSK_LOOP_STAMPS builds only)
     uint32_t *flags;       // per-handle OR of QPSK_STATUS_* raised by this call (or nullptr)
+    int chunked;           // 1: an internal chunk of a longer call (StreamState.tofs runs on)
 };
 
 // One internal chunk's rows appended behind what earlier chunks of the same
@@ -62,6 +63,8 @@ struct AppendArgs {
     const int64_t *counts;       // [2][S]: this chunk's n_bits, n_syms
     int64_t *acc;                // [2][S]: running totals
     int first;
+    int last;                    // the call's last chunk: StreamState.tofs back to 0
+    StreamState *state;
     int S;
 };
 

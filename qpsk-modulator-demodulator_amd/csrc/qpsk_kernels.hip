@@ -392,6 +392,7 @@ __global__ __launch_bounds__(256) void append_rows_kernel(AppendArgs a) {
     if (threadIdx.x == 0) {
         a.acc[s] = off + nb;
         a.acc[a.S + s] = offs + ns;
+        if (a.last) a.state[s].tofs = 0;   // streams whose samples ended earlier included
     }
 }
 

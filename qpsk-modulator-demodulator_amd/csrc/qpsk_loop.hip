@@ -291,9 +291,16 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         f2 *row = L.mf + lane * kRowS;
         // taps x[b-1..b+2] of physical index b: contiguous thanks to the mirror
         auto taps = [&](int b) -> const f2 * { return row + kMir - 3 + ((b + 2) & (kRing - 1)); };
-        // the same address straight from floor(t): fl + (1.5*2^52 + d + 2) holds
+        // Timing runs in the reference's coordinates: t = baseIndex + mu with
+        // baseIndex counted from the start of the whole DeModulate call's queue
+        // (MuellerMuller.cs:113-115 rounds newTime at that magnitude).  P = the
+        // queue index of this chunk's first sample (0 unless the call was split
+        // into internal chunks); physical index b = floor(t) - P + d.
+        const int P = mine ? static_cast<int>(st.tofs) : 0;
+        const int dP = d - P;
+        // the same address straight from floor(t): fl + (1.5*2^52 + dP + 2) holds
         // b + 2 in its low mantissa bits (no float->int conversion on the chain)
-        const double tap_shift = 6755399441055744.0 + static_cast<double>(d + 2);
+        const double tap_shift = 6755399441055744.0 + static_cast<double>(dP + 2);
         // loop-invariant LDS address of x[-3] relative to the ring, kept opaque so
         // the whole base lives in one VGPR and the tap reads use immediate offsets
         typedef __attribute__((address_space(3))) const f2 lds_f2;
@@ -324,7 +331,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         // logical time baseIndex + mu.  After baseIndex = floor(t), mu = t - baseIndex
         // (exact, Sterbenz), (double)baseIndex + mu == t exactly, so the reference's
         // next time baseIndex + mu + advance (MuellerMuller.cs:113) is simply t + advance
-        double nt = static_cast<double>(base - d) + mu;
+        double nt = static_cast<double>(base - dP) + mu;
         // the TED reuses the previous symbol widened to double and the decisions
         // as doubles +-1.0: d*x is exact, so fma(d1, x1, d2*x2) rounds the same
         // exact sum as the reference's (double)d1*x1 + (double)d2*x2
@@ -377,7 +384,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 nt = nt + adv;
                 const double fl = floor(nt);
                 mu = nt - fl;
-                base = static_cast<int>(fl) + d;
+                base = static_cast<int>(fl) + dP;
                 if constexpr (decltype(load)::value) {
                     tp = taps_fl(fl);
                     xm1 = tp[0]; x0 = tp[1]; x1 = tp[2]; x2 = tp[3];
@@ -433,7 +440,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             // ring and opens the next round, so the wave-wide count settles at
             // the symbol rate and no per-lane remainder runs in steady state.
             {
-                const double room = static_cast<double>(rend - d - 3) - nt;
+                const double room = static_cast<double>(rend - dP - 3) - nt;
                 const double step_max = sps + 0.1;
                 const int cap_l = kmax - k;
                 // streams whose samples end in this round vote too; streams that
@@ -480,7 +487,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const bool last = cnt <= (r + 1) * KB;
                 auto more = [&]() {
                     return (base + 2 < rend) & (k < kmax) &
-                           (last | (static_cast<double>(rend - d - 3) - nt >= lag_max));
+                           (last | (static_cast<double>(rend - dP - 3) - nt >= lag_max));
                 };
                 if (__builtin_amdgcn_ballot_w64(more()) != 0) {   // one vote skips the loop in steady state
                     reload();                   // the uniform loop ended on a tap-less step
@@ -552,6 +559,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         StreamState *g = a.state + s;
         g->base = lbase - consumed;
         g->carry_n = keep;
+        g->tofs = a.chunked ? static_cast<int64_t>(P) + consumed : 0;
         g->mu = mu;
         g->integ = integ;
         // the widened registers hold the reference's floats exactly

@@ -72,6 +72,8 @@ int dev_alloc(T **p, size_t count) {
 
 constexpr int kEv = 6;
 constexpr int64_t kMaxSamplesPerCall = int64_t(1) << 30;
+// the symbol loop keeps sample indices of one call in 32-bit integers
+constexpr int64_t kMaxCallSamples = (int64_t(1) << 31) - 129;
 }  // namespace
 
 namespace qpsk {
@@ -202,6 +204,8 @@ int validate(qpsk_demod *h, Call &c) {
         if (c.n_samples < 0) return fail(QPSK_ERR_ARGUMENT, "negative n_samples");
         n_call = c.n_samples;
     }
+    if (n_call > kMaxCallSamples)
+        return fail(QPSK_ERR_OUT_OF_RANGE, "calls above 2^31 - 129 samples per stream (a C# span holds 2^30)");
     if (n_call > 0 && !c.iq) return fail(QPSK_ERR_ARGUMENT_NULL, "SamplesIQ is null");
     if (n_call > 0 && c.stride_floats < 2 * n_call) return fail(QPSK_ERR_ARGUMENT, "stride too small");
     if (c.mode == QPSK_MODE_DEMODULATE && (!c.bits || !c.n_bits))
@@ -301,6 +305,7 @@ int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipS
     la.n_syms = h->d_counts + S;
     la.S = S;
     la.flags = h->d_flags + (c.mem == QPSK_MEM_HOST && !c.append ? 1 : 0);
+    la.chunked = c.append ? 1 : 0;
     launch_loop(la, h->lp, c.mode, h->loop_variant, st);
     HIP_TRY(hipGetLastError());
     EV(5, st);
@@ -317,6 +322,8 @@ int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipS
         aa.counts = h->d_counts;
         aa.acc = h->d_acc;
         aa.first = c.first ? 1 : 0;
+        aa.last = c.last ? 1 : 0;
+        aa.state = h->d_state;
         aa.S = S;
         launch_append(aa, st);
         HIP_TRY(hipGetLastError());

@@ -35,6 +35,10 @@ struct alignas(16) StreamState {
     float fll_phase, fll_freq;
     int32_t fll_pos;    // FLL delay-line write position
     int32_t error;      // sticky: 1 = carry overflow
+    int64_t tofs;       // inside a call split into internal chunks: index of this
+                        // chunk's queue start in the whole call's M&M queue, so
+                        // the timing arithmetic runs at the reference's absolute
+                        // baseIndex (0 between calls)
 };
 
 struct LoopParams {
