@@ -75,6 +75,11 @@ template <int KB> struct Ring {
 constexpr int kCapAny = 80;
 constexpr int kCapSps2 = 40;
 constexpr int kCap128Sps2 = 72;
+// sps >= 4 / >= 8: the same backlog limit (lag_max = KB/2) with fewer symbol
+// slots, so the workgroup's LDS drops from 143.5 KB to 125 KB / 104 KB and a
+// matched-filter workgroup of the next pipelined call fits beside it
+constexpr int kCapSps4 = 28;
+constexpr int kCapSps8 = 14;
 typedef double d2 __attribute__((ext_vector_type(2)));
 
 // M&M -> Costas symbol slots: doubles (default; the M&M wave has them widened
@@ -830,6 +835,10 @@ void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant,
         launch_loop_spw<16, kCapSps2, 64>(a, P, mode, stream);
     else if (variant == 3)
         launch_loop_spw<16, kCap128Sps2, 128>(a, P, mode, stream);
+    else if (P.sps >= 8.0)
+        launch_loop_spw<32, kCapSps8, 64>(a, P, mode, stream);
+    else if (P.sps >= 4.0)
+        launch_loop_spw<32, kCapSps4, 64>(a, P, mode, stream);
     else
         launch_loop_spw<32, kCapSps2, 64>(a, P, mode, stream);
 }

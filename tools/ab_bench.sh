@@ -6,7 +6,7 @@ set -e
 rounds=$1; shift
 for i in $(seq 1 "$rounds"); do
   for lib in qpsk-modulator-demodulator_amd/_build/ab/lib*.so; do
-    out=$(QPSK_DEMOD_LIB=$PWD/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-framer --no-parity "$@")
+    out=$(QPSK_DEMOD_LIB=$PWD/$lib timeout -k 10 300 python bench.py --timed-only "$@")
     echo "$(basename "$lib") $(echo "$out" | grep -o '"fir": [0-9.]*') $(echo "$out" | grep -o '"loop": [0-9.]*') $(echo "$out" | grep -o '"value": [0-9.]*')"
   done
 done
