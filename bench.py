@@ -725,6 +725,12 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
 
+    # the JSON line is the only thing on stdout: native libraries (gloo, HIP)
+    # print to fd 1 too, so fd 1 points at stderr until the line is written
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
 
@@ -755,8 +761,9 @@ def main():
         out["sub_records"] = sub
     if world > 1 and not args.no_split_gather:
         out["split_gather"] = split_gather_leg(args, rank, world, dev)
+    sys.stdout.flush()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if world > 1:
         dist.destroy_process_group()
 
