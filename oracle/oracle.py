@@ -50,7 +50,12 @@ class DemodCfg(C.Structure):
         ("lanes", C.c_int),
         ("trig_mode", C.c_int),
         ("ring_capacity", C.c_long),
+        ("iq_balance", C.c_int),
     ]
+
+
+class IQB(C.Structure):
+    _fields_ = [("avg_re", C.c_float), ("avg_im", C.c_float)]
 
 
 def build():
@@ -122,6 +127,7 @@ def lib():
         L.or_nco_free.argtypes = [C.c_void_p]
         L.or_nco_next.argtypes = [C.c_void_p, _f64p, _f64p]
         L.or_apply_lo_pair.argtypes = [C.c_void_p, C.c_void_p, _f32p, C.c_long]
+        L.or_iqb_process.argtypes = [C.POINTER(IQB), _f32p, _f32p, C.c_long, C.c_int]
         L.or_sincos_batch.argtypes = [_f64p, C.c_long, _f64p, _f64p]
         _lib = L
     return _lib
@@ -227,7 +233,8 @@ class OracleFLL:
 
 def demod_cfg(sample_rate, symbol_rate, rrc_alpha=0.9, rrc_span=6, symbol_sync_bw=0.0001,
               costas_loop_bw=120.0, cfo_loop_bw=None, differential=True, tsc=None,
-              enable_fll=False, lanes=8, trig=TRIG_PORTABLE, ring_capacity=300_000_000):
+              enable_fll=False, lanes=8, trig=TRIG_PORTABLE, ring_capacity=300_000_000,
+              iq_balance=False):
     c = DemodCfg()
     lib().or_demod_cfg_default(C.byref(c), int(sample_rate), int(symbol_rate))
     c.rrc_alpha = float(np.float32(rrc_alpha))
@@ -242,6 +249,7 @@ def demod_cfg(sample_rate, symbol_rate, rrc_alpha=0.9, rrc_span=6, symbol_sync_b
     c.lanes = int(lanes)
     c.trig_mode = int(trig)
     c.ring_capacity = int(ring_capacity)
+    c.iq_balance = 1 if iq_balance else 0
     return c
 
 
@@ -257,15 +265,31 @@ def _raise(n):
                          "(MuellerMuller.cs:113-115, 164)")
 
 
+class OracleIQBalancer:
+    """IQ_Balancer (IQ Balancer.cs:10-26); literal=True keeps the reference's
+    loop bound (the first half of the complex samples, the rest of OUT left as
+    it was: zeros here)."""
+
+    def __init__(self):
+        self._st = IQB(0.0, 0.0)
+
+    def process(self, x_iq, literal=False):
+        x = _f32(x_iq)
+        y = np.zeros_like(x)
+        lib().or_iqb_process(C.byref(self._st), _fp(x), _fp(y), x.size, 1 if literal else 0)
+        return y
+
+
 class OracleDemod:
     """QPSKDeModulator restated (QPSKDeModulator.cs:11-457)."""
 
     def __init__(self, sample_rate, symbol_rate, rrc_alpha=0.9, rrc_span=6, symbol_sync_bw=0.0001,
                  costas_loop_bw=120.0, cfo_loop_bw=None, differential=True, tsc=None,
-                 enable_fll=False, lanes=8, trig=TRIG_PORTABLE, ring_capacity=300_000_000):
+                 enable_fll=False, lanes=8, trig=TRIG_PORTABLE, ring_capacity=300_000_000,
+                 iq_balance=False):
         self._cfg = demod_cfg(sample_rate, symbol_rate, rrc_alpha, rrc_span, symbol_sync_bw,
                               costas_loop_bw, cfo_loop_bw, differential, tsc, enable_fll, lanes,
-                              trig, ring_capacity)
+                              trig, ring_capacity, iq_balance)
         self._tsc_keep = self._cfg.tsc
         err = C.c_int()
         self._h = lib().or_demod_new(C.byref(self._cfg), C.byref(err))

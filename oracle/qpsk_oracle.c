@@ -354,6 +354,21 @@ long or_mm_process(or_mm *m, const float *in_iq, long n_floats, float *out_iq, l
 }
 
 /* ------------------------------------------------------------------------ */
+/* IQ Balancer.cs:10-26                                                      */
+/* ------------------------------------------------------------------------ */
+void or_iqb_process(or_iqb *b, const float *in_iq, float *out_iq, long n_floats, int literal)
+{
+    const float ratio = 1e-05f;                                   /* :14 */
+    const long end = literal ? n_floats / 2 : n_floats;           /* :17 (i < IN.Length/2) */
+    for (long i = 0; i < end; i += 2) {
+        b->avg_re = ratio * (in_iq[i] - b->avg_re) + b->avg_re;   /* :19-20 */
+        b->avg_im = ratio * (in_iq[i + 1] - b->avg_im) + b->avg_im;
+        out_iq[i] = in_iq[i] - b->avg_re;                         /* :21-22 */
+        out_iq[i + 1] = in_iq[i + 1] - b->avg_im;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
 /* CostasLoopQpsk.cs:19-130                                                  */
 /* ------------------------------------------------------------------------ */
 struct or_costas {
@@ -566,8 +581,9 @@ struct or_demod {
     double mm_sps, kp, ki;
     float *rrc_f32;
     int n_taps;
-    float *tmp_fll, *tmp_rrc, *tmp_sym;
+    float *tmp_fll, *tmp_rrc, *tmp_sym, *tmp_iqb;
     long tmp_cap;
+    or_iqb iqb;
     /* differential decode state (:72-73) */
     int diff_have_prev;
     float prev_i, prev_q;
@@ -670,7 +686,7 @@ void or_demod_free(or_demod *d)
     or_mm_free(d->mm);
     or_costas_free(d->costas);
     free(d->rrc_f32);
-    free(d->tmp_fll); free(d->tmp_rrc); free(d->tmp_sym);
+    free(d->tmp_fll); free(d->tmp_rrc); free(d->tmp_sym); free(d->tmp_iqb);
     free(d->ring);
     free(d->carry);
     free(d->bits);
@@ -699,6 +715,7 @@ static void ensure_tmp(or_demod *d, long n_floats)               /* :290-302 */
     d->tmp_fll = (float *)realloc(d->tmp_fll, (size_t)p * sizeof(float));
     d->tmp_rrc = (float *)realloc(d->tmp_rrc, (size_t)p * sizeof(float));
     d->tmp_sym = (float *)realloc(d->tmp_sym, (size_t)p * sizeof(float));
+    d->tmp_iqb = (float *)realloc(d->tmp_iqb, (size_t)p * sizeof(float));
     d->tmp_cap = p;
 }
 
@@ -709,8 +726,12 @@ static long demod_core(or_demod *d, const float *iq, long n_floats, char *bits, 
 {
     ensure_tmp(d, n_floats);
     const float *src = iq;
+    if (d->cfg.iq_balance) {                                      /* optional pre-stage */
+        or_iqb_process(&d->iqb, src, d->tmp_iqb, n_floats, 0);
+        src = d->tmp_iqb;
+    }
     if (d->cfg.enable_fll) {                                      /* README.md:16 order */
-        or_fll_process(d->fll, iq, d->tmp_fll, n_floats >> 1);
+        or_fll_process(d->fll, src, d->tmp_fll, n_floats >> 1);
         src = d->tmp_fll;
     }
     or_cfir_filter(d->rrc, src, d->tmp_rrc, n_floats >> 1);     /* :360 */
@@ -804,8 +825,12 @@ long or_demod_constellation(or_demod *d, const float *iq, long n_floats, float *
     if (n_floats & 1) return -1;                                  /* :430 */
     ensure_tmp(d, n_floats > 0 ? n_floats : 1);
     const float *src = iq;
+    if (d->cfg.iq_balance) {
+        or_iqb_process(&d->iqb, src, d->tmp_iqb, n_floats, 0);
+        src = d->tmp_iqb;
+    }
     if (d->cfg.enable_fll) {
-        or_fll_process(d->fll, iq, d->tmp_fll, n_floats >> 1);
+        or_fll_process(d->fll, src, d->tmp_fll, n_floats >> 1);
         src = d->tmp_fll;
     }
     or_cfir_filter(d->rrc, src, d->tmp_rrc, n_floats >> 1);

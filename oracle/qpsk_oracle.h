@@ -60,6 +60,12 @@ int or_fll_taps(const or_fll *f, float *lower_iq, float *upper_iq, int cap_float
 void or_fll_state(const or_fll *f, float *phase, float *freq);
 
 /* QPSKDeModulator.cs:11-457 */
+/* IQ_Balancer (IQ Balancer.cs:10-26): a DC blocker, exponential averages of I
+ * and Q with ratio 1e-5f.  literal = 1 keeps the reference loop bound
+ * (i < IN.Length/2 floats: the first half of the complex samples; the rest of
+ * OUT is not written), 0 covers the whole buffer. */
+typedef struct { float avg_re, avg_im; } or_iqb;
+void or_iqb_process(or_iqb *b, const float *in_iq, float *out_iq, long n_floats, int literal);
 typedef struct or_demod or_demod;
 typedef struct or_demod_cfg {
     int sample_rate, symbol_rate;
@@ -72,6 +78,9 @@ typedef struct or_demod_cfg {
     int lanes;             /* Vector<float>.Count (8 on AVX2 x64) */
     int trig_mode;
     long ring_capacity;    /* framer ring bytes; reference uses 300_000_000 (:58) */
+    int iq_balance;        /* 0 = off (the reference constructs IQ_Balancer, :38, but never
+                              calls it); 1 = IQ_Balancer.Process over the whole call before
+                              the FLL / matched filter (loop bound fixed) */
 } or_demod_cfg;
 void or_demod_cfg_default(or_demod_cfg *c, int sample_rate, int symbol_rate);
 /* returns NULL and sets *err (1 = ArgumentOutOfRange from FLL validation) on error */

@@ -80,6 +80,17 @@ struct FllArgs {
     int S;
 };
 
+struct IqbArgs {
+    const float *x;        // [S][x_stride] float2
+    int64_t x_stride;
+    float *y;              // [S][y_stride] float2
+    int64_t y_stride;
+    const int64_t *lengths;
+    int64_t n;
+    StreamState *state;
+    int S;
+};
+
 // Returns true when a specialised tile kernel was used.
 bool launch_fir(const FirArgs &a, const TapsRev &taps, const float *hrev_dev, int T, int W, int S,
                 int64_t n_max, hipStream_t stream);
@@ -87,6 +98,7 @@ void launch_fir_hist(const FirArgs &a, float *hist_new, int H, int S, hipStream_
 void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant,
                  hipStream_t stream);
 void launch_append(const AppendArgs &a, hipStream_t stream);
+void launch_iq_balance(const IqbArgs &a, hipStream_t stream);
 void launch_fll(const FllArgs &a, const FllParams &P, hipStream_t stream);
 void launch_fll_sys(const FllArgs &a, const FllParams &P, hipStream_t stream);   // qpsk_fll.hip
 

@@ -349,6 +349,37 @@ __global__ __launch_bounds__(64) void fll_kernel(FllArgs a, FllParams P) {
 }
 
 // ---------------------------------------------------------------------------
+// IQ_Balancer.Process (IQ Balancer.cs:15-25), the optional pre-stage
+// (qpsk_demod_params.iq_balance): per-stream exponential averages of I and Q
+// subtracted from the samples, in the reference's float order (mul, then add;
+// no fma).  The reference loop stops at IN.Length/2 floats, i.e. half the
+// samples; this stage covers every sample ("fixed").  A
+// serial recurrence: one lane per stream, two samples per 16-B load.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void iq_balance_kernel(IqbArgs a) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.S) return;
+    const int64_t n = a.lengths ? a.lengths[s] : a.n;
+    if (n <= 0) return;
+    const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
+    f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride;
+    const float ratio = 1e-05f;
+    float ar = a.state[s].iqb_re, ai = a.state[s].iqb_im;
+    for (int64_t t = 0; t < n; ++t) {
+        const f2 v = x[t];
+        ar = ratio * (v.x - ar) + ar;
+        ai = ratio * (v.y - ai) + ai;
+        y[t] = f2{v.x - ar, v.y - ai};
+    }
+    a.state[s].iqb_re = ar;
+    a.state[s].iqb_im = ai;
+}
+
+void launch_iq_balance(const IqbArgs &a, hipStream_t stream) {
+    hipLaunchKernelGGL(iq_balance_kernel, dim3((a.S + 63) / 64), dim3(64), 0, stream, a);
+}
+
+// ---------------------------------------------------------------------------
 // Chunked calls: one DeModulate call longer than max_samples_per_call runs as
 // consecutive internal chunks (the chain is chunk-invariant), and each chunk's
 // bit row / symbol row is appended behind the previous chunk's in the

@@ -100,6 +100,7 @@ struct qpsk_demod {
     float *d_hrev = nullptr;
     float *d_in = nullptr;
     float *d_fll_out[2] = {nullptr, nullptr};
+    float *d_iqb = nullptr;          // [S][n_max] float2, IQ_Balancer output (iq_balance only)
     float *d_hist[2] = {nullptr, nullptr};
     int hist_cur = 0;
     float *d_mf[2] = {nullptr, nullptr};
@@ -252,6 +253,17 @@ namespace {
     do {                                               \
         if (ev) HIP_TRY(hipEventRecord(ev[i], (st)));  \
     } while (0)
+
+// optional IQ_Balancer pre-stage (IQ Balancer.cs:15-25) into d_iqb
+void run_iqb(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_len, int64_t n_call,
+             hipStream_t st) {
+    IqbArgs ia{};
+    ia.x = x; ia.x_stride = x_stride;
+    ia.y = h->d_iqb; ia.y_stride = h->n_max;
+    ia.lengths = d_len; ia.n = n_call;
+    ia.state = h->d_state; ia.S = h->S;
+    launch_iq_balance(ia, st);
+}
 
 // FLL (Band-Edge Filter.cs:64-87), README order FLL -> MF
 void run_fll(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_len, int64_t n_call,
@@ -520,6 +532,8 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
         return cleanup_fail(rc);
     if (p->enable_fll && (rc = dev_alloc(&h->d_fll_out[0], static_cast<size_t>(2 * S * h->n_max))))
         return cleanup_fail(rc);
+    if (p->iq_balance && (rc = dev_alloc(&h->d_iqb, static_cast<size_t>(2 * S * h->n_max))))
+        return cleanup_fail(rc);
     if (hipHostMalloc(reinterpret_cast<void **>(&h->h_counts), 2 * S * sizeof(int64_t)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&h->h_flags), sizeof(uint32_t)) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipHostMalloc"));
@@ -561,6 +575,7 @@ int qpsk_demod_destroy(qpsk_demod *h) {
         if (h->e_back[b]) hipEventDestroy(h->e_back[b]);
     }
     hipFree(h->d_carry);
+    hipFree(h->d_iqb);
     hipFree(h->d_state);
     hipFree(h->d_fll_delay);
     hipFree(h->d_bits);
@@ -660,6 +675,11 @@ int process_one(qpsk_demod *h, const Call &c) {
         d_len = h->d_lengths[0];
     }
 
+    if (h->p.iq_balance && n_call > 0) {
+        run_iqb(h, x, x_stride, d_len, n_call, st);
+        x = h->d_iqb;
+        x_stride = h->n_max;
+    }
     if (h->p.enable_fll && n_call > 0) {
         run_fll(h, x, x_stride, d_len, n_call, h->d_fll_out[0], st);
         x = h->d_fll_out[0];
@@ -702,7 +722,13 @@ int process_async_one(qpsk_demod *h, const Call &c) {
     }
     EV(0, F);
     const float *x = iq;
-    const int64_t x_stride = stride_floats / 2;
+    int64_t x_stride = stride_floats / 2;
+    if (h->p.iq_balance && n_call > 0) {
+        // read only by this call's own front stage (FLL or FIR on F)
+        run_iqb(h, x, x_stride, d_len, n_call, F);
+        x = h->d_iqb;
+        x_stride = h->n_max;
+    }
     float *mf;
     if (h->p.enable_fll) {
         // front = FLL into boundary rows b; back = FIR (MF rows 0) + loop

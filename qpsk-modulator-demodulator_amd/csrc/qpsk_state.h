@@ -39,6 +39,7 @@ struct alignas(16) StreamState {
                         // chunk's queue start in the whole call's M&M queue, so
                         // the timing arithmetic runs at the reference's absolute
                         // baseIndex (0 between calls)
+    float iqb_re, iqb_im;   // IQ_Balancer._avgReal, _avgImg (IQ Balancer.cs:13)
 };
 
 struct LoopParams {

@@ -62,7 +62,8 @@ class DemodParams(C.Structure):
         ("device", C.c_int32),
         ("max_samples_per_call", C.c_int64),
         ("loop_variant", C.c_int32),
-        ("reserved", C.c_int32 * 7),
+        ("iq_balance", C.c_int32),
+        ("reserved", C.c_int32 * 6),
     ]
 
 
@@ -236,7 +237,7 @@ def _check(rc):
 def params(sample_rate, symbol_rate, rrc_alpha=0.9, rrc_span=6, symbol_sync_bandwidth=0.0001,
            costas_loop_bandwidth=120.0, cfo_loop_bandwidth=None, differential=True,
            enable_fll=False, vector_lanes=8, device=0, max_samples_per_call=1 << 20,
-           loop_variant=0):
+           loop_variant=0, iq_balance=False):
     p = DemodParams()
     lib().qpsk_demod_params_init(C.byref(p), int(sample_rate), int(symbol_rate))
     p.rrc_alpha = float(np.float32(rrc_alpha))
@@ -251,6 +252,7 @@ def params(sample_rate, symbol_rate, rrc_alpha=0.9, rrc_span=6, symbol_sync_band
     p.device = int(device)
     p.max_samples_per_call = int(max_samples_per_call)
     p.loop_variant = int(loop_variant)
+    p.iq_balance = 1 if iq_balance else 0
     return p
 
 

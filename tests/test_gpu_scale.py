@@ -264,3 +264,24 @@ def test_modulate_then_demodulate_round_trip():
         sig = m.ModulateTextUtf8(f"frame {k}: " + K.PAYLOAD)
         texts.append(d.DeModulateTextUtf8(sig))
     assert sum(t.endswith(K.PAYLOAD) for t in texts) >= 3
+
+
+@pytest.mark.parametrize("fll", [False, True])
+def test_iq_balance_prestage_bit_exact(fll):
+    """The optional IQ_Balancer pre-stage (IQ Balancer.cs:15-25) on a signal
+    with a DC offset, in ragged chunked calls, sync and pipelined: bits and
+    symbols equal the oracle with the same pre-stage."""
+    S = 3
+    iq = K.batch_signals(S, seed0=700, sps=8, span=8, n_bits=2000, snr_db=18)
+    iq[:, 0::2] += 0.3
+    iq[:, 1::2] -= 0.2
+    n = iq.shape[1] // 2
+    calls = [[n // 3, n // 2, 100], [n - n // 3, n - n // 2, n - 100]]
+    kw = dict(enable_fll=fll, cfo_loop_bandwidth=1e-3) if fll else {}
+    okw = dict(enable_fll=fll, cfo_loop_bw=1e-3) if fll else {}
+    got = gpu_run(iq, calls, 8, 8, iq_balance=True, **kw)
+    ref = oracle_run(iq, calls, 8, 8, iq_balance=True, **okw)
+    assert_same(got, ref)
+    from test_gpu_parity import async_run
+    got_async, _ = async_run(iq, calls, 8, 8, iq_balance=True, **kw)
+    assert_same(got_async, ref)

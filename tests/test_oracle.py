@@ -162,3 +162,28 @@ def test_fll_float_trig_equals_glibc(tmp_path):
                            "-o", exe, os.path.join(root, "tools", "check_glibc_sincosf.c"), "-lm"])
     out = subprocess.run([exe, "3"], capture_output=True, text=True).stdout
     assert out.strip().endswith(" 0 differ"), out
+
+
+def test_iq_balancer_restatement():
+    """IQ_Balancer.Process (IQ Balancer.cs:15-25) against a float32 numpy
+    model: the literal loop stops at IN.Length/2 floats (half the samples),
+    the fixed one covers all; the averages carry across calls."""
+    rng = np.random.default_rng(4)
+    x = (rng.standard_normal(64) + 0.5).astype(np.float32)
+    ratio = np.float32(1e-05)
+
+    def model(v, n_floats, ar, ai):
+        out = np.zeros_like(v)
+        for i in range(0, n_floats, 2):
+            ar = np.float32(ratio * np.float32(v[i] - ar)) + ar
+            ai = np.float32(ratio * np.float32(v[i + 1] - ai)) + ai
+            ar, ai = np.float32(ar), np.float32(ai)
+            out[i], out[i + 1] = v[i] - ar, v[i + 1] - ai
+        return out, ar, ai
+
+    lit, _, _ = model(x, x.size // 2, np.float32(0), np.float32(0))
+    assert np.array_equal(O.OracleIQBalancer().process(x, literal=True), lit)
+    b = O.OracleIQBalancer()
+    y1, y2 = b.process(x[:20]), b.process(x[20:])
+    full, _, _ = model(x, x.size, np.float32(0), np.float32(0))
+    assert np.array_equal(np.concatenate([y1, y2]), full)

@@ -20,7 +20,8 @@ STATE = np.dtype([("mu", "f8"), ("integ", "f8"), ("theta", "f8"), ("freq", "f8")
                   ("has_prev", "i4"), ("psi", "f4"), ("psq", "f4"), ("pdi", "f4"), ("pdq", "f4"),
                   ("carry_n", "i4"), ("diff_have", "i4"), ("diff_pi", "f4"), ("diff_pq", "f4"),
                   ("fll_phase", "f4"), ("fll_freq", "f4"), ("fll_pos", "i4"), ("error", "i4"),
-                  ("tofs", "i8")])   # alignas(16): sizeof(StreamState) == 96
+                  ("tofs", "i8"), ("iqb_re", "f4"), ("iqb_im", "f4"),
+                  ("_pad", "V8")])   # alignas(16): sizeof(StreamState) == 112
 
 
 def main():
