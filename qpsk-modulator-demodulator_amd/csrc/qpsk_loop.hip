@@ -109,7 +109,9 @@ __device__ __forceinline__ int wave_max_i32(int v) {
         const int w = __shfl_xor(v, o, 64);
         v = w > v ? w : v;
     }
-    return v;
+    // every lane holds the maximum now; readfirstlane tells the compiler so,
+    // which keeps loops bounded by it scalar (no exec-mask loop control)
+    return __builtin_amdgcn_readfirstlane(v);
 }
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
@@ -327,7 +329,11 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         };
         // symbols that start in every 64-sample round once a stream is inside its
         // samples: the timing advance is at most sps + 0.1 per symbol
-        const int kguar = static_cast<int>(floor((KB - sps - 4.0) / (sps + 0.1)));
+        const int kguar = __builtin_amdgcn_readfirstlane(static_cast<int>(floor((KB - sps - 4.0) / (sps + 0.1))));
+        // the per-round votes' thresholds (G - 1) * step_max, G = kguar .. kguar + 3
+        const double step_max = sps + 0.1;
+        const double thr0 = (kguar - 1) * step_max, thr1 = kguar * step_max;
+        const double thr2 = (kguar + 1) * step_max, thr3 = (kguar + 2) * step_max;
         // largest backlog (samples behind rend) a stream may carry into the next
         // round: half a round keeps its taps inside the ring slots not being
         // refilled, and a round then holds at most (KB + lag_max + 4)/(sps - 0.1) + 1
@@ -446,21 +452,22 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             // the symbol rate and no per-lane remainder runs in steady state.
             {
                 const double room = static_cast<double>(rend - dP - 3) - nt;
-                const double step_max = sps + 0.1;
                 const int cap_l = kmax - k;
                 // streams whose samples end in this round vote too; streams that
                 // ended earlier, stopped ones and rows past the batch do not
                 const bool live = mine & !stop & (cnt > r * KB);
-                // (bitwise & keeps each vote one compare pair, no branches)
-                auto reaches = [&](int G) { return (room >= (G - 1) * step_max) & (cap_l >= G); };
+                // reaches(G) = room >= (G - 1) step_max and cap_l >= G, i.e.
+                // (G - 1) step_max <= eff = min(room, (cap_l - 1) step_max): the
+                // rounded products of distinct small integers with step_max keep
+                // their order.  Non-voters hold +inf.  Each vote is then one
+                // v_cmp straight into an SGPR mask, and the count is picked with
+                // scalar selects (no VALU <-> SALU round trip per vote)
+                const double eff = live ? __builtin_fmin(room, (cap_l - 1) * step_max) : __builtin_inf();
                 int kg = 0;
-                // the four votes are independent: issue them back to back as SGPR
-                // masks and pick the count with scalar selects (no VALU <-> SALU
-                // round trip per vote on the round's critical path)
-                const uint64_t m0 = __builtin_amdgcn_ballot_w64(live & !reaches(kguar));
-                const uint64_t m1 = __builtin_amdgcn_ballot_w64(live & !reaches(kguar + 1));
-                const uint64_t m2 = __builtin_amdgcn_ballot_w64(live & !reaches(kguar + 2));
-                const uint64_t m3 = __builtin_amdgcn_ballot_w64(live & !reaches(kguar + 3));
+                const uint64_t m0 = __builtin_amdgcn_ballot_w64(!(eff >= thr0));
+                const uint64_t m1 = __builtin_amdgcn_ballot_w64(!(eff >= thr1));
+                const uint64_t m2 = __builtin_amdgcn_ballot_w64(!(eff >= thr2));
+                const uint64_t m3 = __builtin_amdgcn_ballot_w64(!(eff >= thr3));
                 kg = m2 == 0 ? (m3 == 0 ? kguar + 3 : kguar + 2)
                              : (m1 == 0 ? kguar + 1 : (m0 == 0 ? kguar : 0));
                 kg = __builtin_amdgcn_readfirstlane(kg);
@@ -606,7 +613,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         // otherwise each iteration rebuilds some from SGPR halves (VOP3 reads
         // one scalar operand), which costs issue slots on an issue-bound chain
         asm volatile("" : "+v"(ca), "+v"(cb), "+v"(kTwoPi), "+v"(kPi));
-        asm volatile("" : "+v"(K.INV), "+v"(K.SH), "+v"(K.P1), "+v"(K.P2), "+v"(K.P3));
+        asm volatile("" : "+v"(K.INV), "+v"(K.SH), "+v"(K.P1), "+v"(K.P2));
         asm volatile("" : "+v"(K.S3), "+v"(K.S5), "+v"(K.C4), "+v"(K.C6));
 #ifdef QPSK_LOOP_STAMPS
         unsigned long long k_bar = 0, k_loop = 0, k_uni = 0, k_uit = 0;

@@ -190,10 +190,10 @@ def portable_sincos(x):
         if math.isnan(x) or math.isinf(x):
             return math.nan, math.nan
         x = math.fmod(x, 6.28318530717958647693)
-    k = float(round(x * float.fromhex("0x1.45f306dc9c883p+6")))  # rint: half-even
+    sh = float.fromhex("0x1.8p+52")
+    k = _fma(x, float.fromhex("0x1.45f306dc9c883p+6"), sh) - sh   # rint of the exact product
     r = _fma(-k, float.fromhex("0x1.921fb54442d18p-7"), x)
     r = _fma(-k, float.fromhex("0x1.1a62633145c07p-61"), r)
-    r = _fma(-k, float.fromhex("-0x1.f1976b7ed8fbcp-117"), r)
     ts, ls, tc, lc = SINCOS_TABLE[int(k) & 511]
     z = r * r
     r3p = (r * z) * _fma(z, 1.0 / 120.0, -1.0 / 6.0)

@@ -67,6 +67,41 @@ __global__ void kern(double *out, long long *cyc, int iters) {
             REP64(asm volatile("v_pk_add_f32 %0, %0, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "+v"(pa) : "v"(pb));)
         } else if (V == 19) {  // dependent v_cvt_f32_f64 -> v_pk_mul_f32 (f64 result into packed)
             REP64(asm volatile("v_cvt_f64_f32 %0, %1\n\tv_pk_mul_f32 %2, %2, %3\n\tv_cvt_f32_f64 %1, %0" : "+v"(a), "+v"(fa), "+v"(pa) : "v"(pb));)
+        } else if (V == 20) {  // 4 independent v_mul_f64 chains
+            REP8(REP8(asm volatile("v_mul_f64 %0, %0, %4\n\tv_mul_f64 %1, %1, %4\n\t"
+                                   "v_mul_f64 %2, %2, %4\n\tv_mul_f64 %3, %3, %4"
+                                   : "+v"(a), "+v"(d), "+v"(e), "+v"(f) : "v"(b));))
+        } else if (V == 21) {  // 4 independent v_add_f64 chains
+            REP8(REP8(asm volatile("v_add_f64 %0, %0, %4\n\tv_add_f64 %1, %1, %4\n\t"
+                                   "v_add_f64 %2, %2, %4\n\tv_add_f64 %3, %3, %4"
+                                   : "+v"(a), "+v"(d), "+v"(e), "+v"(f) : "v"(b));))
+        } else if (V == 22) {  // 4 independent fma_f64 chains, lanes 0..31 only
+            if (threadIdx.x % 64 < 32) {
+                REP8(REP8(asm volatile("v_fma_f64 %0, %0, %4, %5\n\tv_fma_f64 %1, %1, %4, %5\n\t"
+                                       "v_fma_f64 %2, %2, %4, %5\n\tv_fma_f64 %3, %3, %4, %5"
+                                       : "+v"(a), "+v"(d), "+v"(e), "+v"(f) : "v"(b), "v"(c));))
+            }
+        } else if (V == 23) {  // 2 independent fma_f64 chains + 2 independent add_u32 chains
+            int ic = ia;
+            REP8(REP8(asm volatile("v_fma_f64 %0, %0, %4, %5\n\tv_add_u32 %2, %2, %6\n\t"
+                                   "v_fma_f64 %1, %1, %4, %5\n\tv_add_u32 %3, %3, %6"
+                                   : "+v"(a), "+v"(d), "+v"(ia), "+v"(ic) : "v"(b), "v"(c), "v"(ib));))
+            ia += ic;
+        } else if (V == 24) {  // 4 independent v_mov_b64
+            REP8(REP8(asm volatile("v_mov_b64 %0, %4\n\tv_mov_b64 %1, %4\n\t"
+                                   "v_mov_b64 %2, %4\n\tv_mov_b64 %3, %4"
+                                   : "=v"(a), "=v"(d), "=v"(e), "=v"(f) : "v"(b));))
+        } else if (V == 25) {  // 4 independent v_cmp_le_f64 -> distinct SGPR pairs
+            unsigned long long m0, m1, m2, m3;
+            REP8(REP8(asm volatile("v_cmp_le_f64 %0, %4, %5\n\tv_cmp_le_f64 %1, %4, %6\n\t"
+                                   "v_cmp_le_f64 %2, %5, %6\n\tv_cmp_le_f64 %3, %6, %4"
+                                   : "=s"(m0), "=s"(m1), "=s"(m2), "=s"(m3) : "v"(a), "v"(b), "v"(c));))
+            ia += (int)(m0 + m1 + m2 + m3);
+        } else if (V == 26) {  // dependent f64 chain: mul, add, add (kb -> k shape)
+            REP8(REP8(asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));))
+            REP8(REP8(asm volatile("v_add_f64 %0, %0, %1" : "+v"(d) : "v"(b));))
+        } else if (V == 27) {  // ds_read_b128 dependent chain (address from data)
+            REP64(asm volatile("ds_read_b128 v[100:103], %0\n\ts_waitcnt lgkmcnt(0)\n\tv_mov_b32 %0, v100" : "+v"(addr) :: "v100", "v101", "v102", "v103");)
         } else if (V == 12) {  // scalar op stream (s_mov: leaves SCC, which the loop branch uses, alone)
             int sa = it, sb = 7;
             REP64(asm volatile("s_mov_b32 %0, %1" : "=s"(sa) : "s"(sb));)
@@ -87,7 +122,9 @@ int main() {
                            "dep mul_f64", "fma_f64 + cndmask", "dep floor_f64",
                            "cvt f32<->f64 pair", "dep add_f64", "scalar s_add", "dep pk_add_f32",
                            "dep pk_mul_f32", "dep add_f32", "dep add_f32_dpp+nop1", "4x indep pk_add",
-                           "dep pk_add opsel/neg", "cvt>pk_mul>cvt"};
+                           "dep pk_add opsel/neg", "cvt>pk_mul>cvt", "4x indep mul_f64", "4x indep add_f64",
+                           "4x indep fma_f64 32 lanes", "2 fma_f64 + 2 add_u32", "4x v_mov_b64",
+                           "4x v_cmp_le_f64", "fma_f64 chain + add_f64 chain (seq)", "dep ds_read_b128+mov"};
     const int iters = 1000;
     auto run = [&](auto kfn, int idx, int waves_per_block, int blocks) {
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * waves_per_block), 0, 0, out, cyc, 10);
@@ -105,6 +142,9 @@ int main() {
         run(kern<12>, 12, w, 1); run(kern<13>, 13, w, 1); run(kern<14>, 14, w, 1);
         run(kern<15>, 15, w, 1); run(kern<16>, 16, w, 1); run(kern<17>, 17, w, 1);
         run(kern<18>, 18, w, 1); run(kern<19>, 19, w, 1);
+        run(kern<20>, 20, w, 1); run(kern<21>, 21, w, 1); run(kern<22>, 22, w, 1);
+        run(kern<23>, 23, w, 1); run(kern<24>, 24, w, 1); run(kern<25>, 25, w, 1);
+        run(kern<26>, 26, w, 1); run(kern<27>, 27, w, 1);
     }
     // s_memtime rate: ticks over a wall-clock interval
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);

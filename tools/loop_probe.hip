@@ -51,12 +51,12 @@ int main(int argc, char** argv) {
   hipMalloc(&carry, S * kCarryMax * 8); hipMemset(carry, 0, S * kCarryMax * 8);
   std::vector<StreamState> hs(S); for (auto& x : hs) { x = StreamState{}; x.base = 1; }
   hipMalloc(&st, S * sizeof(StreamState)); hipMemcpy(st, hs.data(), S * sizeof(StreamState), hipMemcpyHostToDevice);
-  const int64_t words = n / 8;
+  const int64_t words = n / 2;
   hipMalloc(&bits, S * words * 4); hipMalloc(&cnt, 2 * S * 8); hipMalloc(&probe, 16 * S * 8);
   hipMemset(probe, 0, 16 * S * 8);
   LoopArgs a{}; a.mf = mf; a.mf_stride = stride; a.carry = carry; a.n = n; a.state = st; a.bits = bits;
   a.bits_stride_words = words; a.bits_cap_words = words; a.n_bits = cnt; a.n_syms = cnt + S; a.S = S; a.probe = probe;
-  LoopParams P{}; P.sps = 8.0; P.kp = 2.622462326512427e-3; P.ki = 3.443172085385801e-06; P.c_alpha = 0.13751550967894244; P.c_beta = 0.010184293139132996; P.differential = 1;
+  LoopParams P{}; P.sps = argc > 6 ? atof(argv[6]) : 8.0; P.kp = 2.622462326512427e-3; P.ki = 3.443172085385801e-06; P.c_alpha = 0.13751550967894244; P.c_beta = 0.010184293139132996; P.differential = 1;
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   const int burn = argc > 4 ? atoi(argv[4]) : 0;
   hipStream_t bs; hipStreamCreateWithFlags(&bs, hipStreamNonBlocking);
