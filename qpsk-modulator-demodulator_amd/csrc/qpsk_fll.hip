@@ -48,6 +48,7 @@
 namespace qpsk {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr int kSysStreams = 32;          // streams per 256-thread block: 8 per wave
 constexpr int kRingLen = 64;             // mixed samples per stream: x[t] at t & 63 and (t & 63) + 64
@@ -138,7 +139,11 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
     typedef __attribute__((address_space(3))) f2 lds_f2;
     uint32_t ring_addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_f2 *)(L.ring + g * kRingRow)));
     asm volatile("" : "+v"(ring_addr));
-    lds_f2 *ring = reinterpret_cast<lds_f2 *>(static_cast<uintptr_t>(ring_addr));
+    // rows are 1040 B apart from a 16-B aligned base: telling the compiler lets it
+    // pair the ring accesses into ds_read2_b64 / ds_write2_b64 (the opaque base
+    // alone hides the alignment)
+    lds_f2 *ring = reinterpret_cast<lds_f2 *>(
+        __builtin_assume_aligned(reinterpret_cast<lds_f2 *>(static_cast<uintptr_t>(ring_addr)), 16));
     const f2 *x = reinterpret_cast<const f2 *>(a.x) + sv * a.x_stride;
     f2 *y = reinterpret_cast<f2 *>(a.y) + sv * a.y_stride;
 
@@ -186,26 +191,31 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
         }
     }
     // partial accumulators of the step at time t (inputs x[t-32], x[t-24],
-    // x[t-16], x[t-8]); rb = ring + ((t - 32) & 63) - off, off <= 8, so the
-    // four reads are static offsets (the mirror covers the wrap)
+    // x[t-16], x[t-8]); fetch(k) = x[(t - off) - 32 + k], off <= 8: from the ring
+    // (rb = ring + ((t - off - 32) & 63), static offsets, the mirror covers the
+    // wrap) or from a block's register window
     f2 PR, PI;
-    auto partial = [&](const lds_f2 *rb, int off) __attribute__((always_inline)) {
+    auto partial = [&](auto fetch, int off) __attribute__((always_inline)) {
         // the reference starts each lane accumulator at +0 (Vector<float>.Zero);
         // 0 + v differs from v only in the sign of a zero, and the filter
         // outputs are only ever squared (the band powers), so the start is dropped
         f2 ar, ai;
-        band_prod(TA[0], TB[0], rb[off], ar, ai);
+        band_prod(TA[0], TB[0], fetch(off), ar, ai);
 #pragma unroll
         for (int j = 1; j < 4; ++j) {
             f2 R, I;
-            band_prod(TA[j], TB[j], rb[off + 8 * j], R, I);
+            band_prod(TA[j], TB[j], fetch(off + 8 * j), R, I);
             ar = ar + R;
             ai = ai + I;
         }
         PR = ar;
         PI = ai;
     };
-    partial(ring + ((0 - 32) & (kRingLen - 1)), 0);
+    auto ring_at = [&](int64_t t0) __attribute__((always_inline)) {
+        const lds_f2 *rb = ring + ((t0 - 32) & (kRingLen - 1));
+        return [rb](int k) -> f2 { return rb[k]; };
+    };
+    partial(ring_at(0), 0);
 
     const float two_pi = 2.0f * 3.14159274101257324219f;
     const float beta = P.beta, alpha = P.alpha, fmax_ = P.max_freq, fmin_ = P.min_freq;
@@ -217,8 +227,13 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
     // max |freq| instead, and the block is redone exactly if either left its
     // range (the phase every ~2pi/|freq| samples, the clamp essentially never),
     // so a block is branch-free straight-line code.
-    auto step = [&](f2 in, int64_t t0, int u, auto first, auto exact, float &amax, float &fmx)
-        __attribute__((always_inline)) {
+    // REG: a uniform block's step -- the partial sums read the block's register
+    // window X (x[t0-32 .. t0-1]; x[t0] is this block's first output, xmv[0])
+    // and the outputs stay in xmv until the block writes them to the ring at its
+    // end (16-B LDS accesses instead of a read per tap and a write pair per
+    // sample); otherwise the ring is read and written per sample
+    auto step = [&](f2 in, int64_t t0, int u, auto first, auto exact, float &amax, float &fmx,
+                    auto reg, const f2 *X, f2 *xmv) __attribute__((always_inline)) {
         // MathF.Cos / MathF.Sin (Band-Edge Filter.cs:108-109) = glibc cosf / sinf
         float sn, cs;
         if constexpr (decltype(first)::value) {
@@ -235,9 +250,13 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
         const f2 csn = f2{cs, sn};
         // (inI*c - inQ*s, inI*s + inQ*c)
         const f2 xm = add_swap_neglo(mul_xlo(in, csn), mul_xhi(in, csn));
-        lds_f2 *wb = ring + (t0 & (kRingLen - 1));
-        wb[u] = xm;
-        wb[u + kRingLen] = xm;
+        if constexpr (decltype(reg)::value) {
+            xmv[u] = xm;
+        } else {
+            lds_f2 *wb = ring + (t0 & (kRingLen - 1));
+            wb[u] = xm;
+            wb[u + kRingLen] = xm;
+        }
         y[t0 + u] = xm;
         f2 R4, I4;
         band_prod(TA[4], TB[4], xm, R4, I4);
@@ -265,24 +284,49 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
             fmx = fmaxf(fmx, fabsf(freq));
         }
 #if !(QPSK_FLL_PROBE & 2)
-        partial(ring + ((t0 - 32) & (kRingLen - 1)), u + 1);
+        if constexpr (decltype(reg)::value)
+            partial([&](int k) -> f2 { return k == 32 ? xmv[0] : X[k]; }, u + 1);
+        else
+            partial(ring_at(t0), u + 1);
 #endif
     };
     // 8 samples of every stream of the wave, no masks
+    typedef __attribute__((address_space(3))) f4 lds_f4;
     auto block = [&](const f2 *in, int64_t t0, auto first) __attribute__((always_inline)) {
         const float ph0 = phase, fr0 = freq;
         const f2 sr0 = SR, si0 = SI, pr0 = PR, pi0 = PI;
         float amax = 0.f, fmx = 0.f;
-        step(in[0], t0, 0, first, std::false_type{}, amax, fmx);
+        // the window x[t0-32 .. t0-1]: (t0 - 32) & 63 is a multiple of 8 samples,
+        // so 16 aligned 16-B reads (the mirror keeps it contiguous)
+        f2 X[32], xmv[8];
+        const lds_f4 *wr = reinterpret_cast<const lds_f4 *>(ring + ((t0 - 32) & (kRingLen - 1)));
 #pragma unroll
-        for (int u = 1; u < 8; ++u) step(in[u], t0, u, std::false_type{}, std::false_type{}, amax, fmx);
+        for (int k = 0; k < 16; ++k) {
+            const f4 v = wr[k];
+            X[2 * k] = f2{v.x, v.y};
+            X[2 * k + 1] = f2{v.z, v.w};
+        }
+        step(in[0], t0, 0, first, std::false_type{}, amax, fmx, std::true_type{}, X, xmv);
+#pragma unroll
+        for (int u = 1; u < 8; ++u)
+            step(in[u], t0, u, std::false_type{}, std::false_type{}, amax, fmx, std::true_type{}, X, xmv);
         if (!(QPSK_FLL_PROBE & 8) && __builtin_expect(__ballot((amax > two_pi) | (fmx > fmax_)) != 0, 0)) {
             // some stream's phase needed a wrap or its frequency a clamp: redo
-            // from the block start (its ring slots and outputs are rewritten)
+            // from the block start (its outputs are rewritten)
             phase = ph0; freq = fr0; SR = sr0; SI = si0; PR = pr0; PI = pi0;
-            step(in[0], t0, 0, first, std::true_type{}, amax, fmx);
+            step(in[0], t0, 0, first, std::true_type{}, amax, fmx, std::true_type{}, X, xmv);
 #pragma unroll
-            for (int u = 1; u < 8; ++u) step(in[u], t0, u, std::false_type{}, std::true_type{}, amax, fmx);
+            for (int u = 1; u < 8; ++u)
+                step(in[u], t0, u, std::false_type{}, std::true_type{}, amax, fmx, std::true_type{}, X, xmv);
+        }
+        // the block's outputs into the ring and its mirror: x[t0 .. t0+7] at
+        // t0 & 63, a multiple of 8 samples (64-B aligned)
+        lds_f4 *ww = reinterpret_cast<lds_f4 *>(ring + (t0 & (kRingLen - 1)));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const f4 v = f4{xmv[2 * k].x, xmv[2 * k].y, xmv[2 * k + 1].x, xmv[2 * k + 1].y};
+            ww[k] = v;
+            ww[k + kRingLen / 2] = v;
         }
     };
 
@@ -342,8 +386,12 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
 #pragma unroll
             for (int u = 0; u < 8; ++u)
                 if (t0 + u < n) {
-                    if (t0 + u == 0) step(cur[u], t0, u, std::true_type{}, std::true_type{}, amax, fmx);
-                    else step(cur[u], t0, u, std::false_type{}, std::true_type{}, amax, fmx);
+                    if (t0 + u == 0)
+                        step(cur[u], t0, u, std::true_type{}, std::true_type{}, amax, fmx, std::false_type{},
+                             nullptr, nullptr);
+                    else
+                        step(cur[u], t0, u, std::false_type{}, std::true_type{}, amax, fmx, std::false_type{},
+                             nullptr, nullptr);
                 }
         }
     }

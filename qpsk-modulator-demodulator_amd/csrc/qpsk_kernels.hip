@@ -77,9 +77,9 @@ __device__ __forceinline__ f2 fir_exact_one(XF x, const float *hrev, int T, int 
     return f2{ai, aq};
 }
 
-template <int T, int W, int Q, bool VEC>
-__global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRev taps, const float *hrev) {
-    constexpr int TILE = kFirThreads * Q;
+template <int T, int W, int Q, bool VEC, int NT>
+__global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, TapsRev taps, const float *hrev) {
+    constexpr int TILE = NT * Q;
     constexpr int NIN = TILE + T - 1;
     constexpr int J = T / W;          // full Vector<float> blocks
     constexpr int NVEC = J * W;
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRe
     const int64_t g0 = tile0 - (T - 1);
     if constexpr (VEC) {
         // g0 is even (T odd) and rows are 16-B aligned: one float4 = 2 samples.
-        for (int p = tid; p < (NIN + 1) / 2; p += kFirThreads) {
+        for (int p = tid; p < (NIN + 1) / 2; p += NT) {
             const int64_t g = g0 + 2 * p;
             f4 v;
             if (g >= 0 && g + 1 < n) {
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRe
             *reinterpret_cast<f4 *>(&lds[lds_slot(2 * p)]) = v;
         }
     } else {
-        for (int i = tid; i < NIN; i += kFirThreads) {
+        for (int i = tid; i < NIN; i += NT) {
             const int64_t g = g0 + i;
             lds[lds_slot(i)] = g < 0 ? hist[T - 1 + g] : (g < n ? x[g] : f2{0.f, 0.f});
         }
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRe
     auto nonfinite = [](float v) -> int { return __builtin_amdgcn_classf(v, 0x207); };   // NaN, +-Inf
     f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride + a.y_offset;
     if constexpr (VEC) {
-        for (int p = tid; p < TILE / 2; p += kFirThreads) {
+        for (int p = tid; p < TILE / 2; p += NT) {
             const int64_t g = tile0 + 2 * p;
             const f4 v = *reinterpret_cast<const f4 *>(&lds[lds_slot(2 * p)]);
             bad |= nonfinite(v.x) | nonfinite(v.y) | nonfinite(v.z) | nonfinite(v.w);
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(kFirThreads) void fir_tile_kernel(FirArgs a, TapsRe
             }
         }
     } else {
-        for (int i = tid; i < TILE; i += kFirThreads) {
+        for (int i = tid; i < TILE; i += NT) {
             const int64_t g = tile0 + i;
             const f2 v = lds[lds_slot(i)];
             bad |= nonfinite(v.x) | nonfinite(v.y);
@@ -434,16 +434,25 @@ void launch_append(const AppendArgs &a, hipStream_t stream) {
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
+template <int T, int NT>
+static void launch_fir_w8_nt(const FirArgs &a, const TapsRev &taps, const float *hrev, int S,
+                             int64_t n_max, bool vec, hipStream_t stream) {
+    constexpr int Q = 8;
+    const int64_t tiles = (n_max + NT * Q - 1) / (NT * Q);
+    dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(S));
+    if (vec)
+        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, true, NT>), grid, dim3(NT), 0, stream, a, taps, hrev);
+    else
+        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, false, NT>), grid, dim3(NT), 0, stream, a, taps, hrev);
+}
+
 template <int T>
 static bool launch_fir_w8(const FirArgs &a, const TapsRev &taps, const float *hrev, int S,
                           int64_t n_max, bool vec, hipStream_t stream) {
-    constexpr int Q = 8;
-    const int64_t tiles = (n_max + kFirThreads * Q - 1) / (kFirThreads * Q);
-    dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(S));
-    if (vec)
-        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, true>), grid, dim3(kFirThreads), 0, stream, a, taps, hrev);
-    else
-        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, false>), grid, dim3(kFirThreads), 0, stream, a, taps, hrev);
+    // 2048-output tiles; 1024- and 512-output tiles (128 / 64 threads, more
+    // workgroups beside the loop kernel's) measured the same at C3 and C2
+    // (pipelined bench, A/B x2 on one MI355X)
+    launch_fir_w8_nt<T, kFirThreads>(a, taps, hrev, S, n_max, vec, stream);
     return true;
 }
 

@@ -136,7 +136,13 @@ QPSK_HDF static inline void qpsk_sincosf_glibc_fast(float y, float *s, float *c)
     const int n = ((int32_t)r + 0x800000) >> 24;
     const double x = fma(-(double)n, 0x1.921FB54442D18p0, (double)y);
     const double x2 = x * x;
-    const double xs = ((n + 1) & 2) ? -x : x;
+    /* The quadrant logic as bit operations on n (fewer instructions on the
+     * FLL's per-sample chain than compares and selects; the same bits):
+     * xs = -x when (n + 1) & 2 -- bit 1 of n + 1 moved into x's sign bit */
+    union { double d; uint64_t u; } xb;
+    xb.d = x;
+    xb.u ^= (uint64_t)(((uint32_t)n + 1u) << 30 & 0x80000000u) << 32;
+    const double xs = xb.d;
     const double x3 = xs * x2;
     const double s1 = fma(x2, -0x1.994eb3774cf24p-13, 0x1.1107605230bc4p-7);
     const double x7 = x3 * x2;
@@ -145,12 +151,18 @@ QPSK_HDF static inline void qpsk_sincosf_glibc_fast(float y, float *s, float *c)
     const double c2 = fma(x2, 0x1.99343027bf8c3p-16, -0x1.6c087e89a359dp-10);
     const double c1 = fma(x2, -0x1.ffffffd0c621cp-2, 0x1p0);
     const double x6 = x4 * x2;
-    double cp = fma(x6, c2, fma(x4, 0x1.55553e1068f19p-5, c1));
-    if (n & 2) cp = -cp;
-    // sin(-0) must stay -0 (glibc returns y below 2^-12); the polynomial's
-    // fma(-0 * S1, -0) is +0
-    const float fs = y == 0.0f ? y : (float)sp, fc = (float)cp;
-    *s = (n & 1) ? fc : fs;
-    *c = (n & 1) ? fs : fc;
+    const double cp = fma(x6, c2, fma(x4, 0x1.55553e1068f19p-5, c1));
+    /* glibc negates cp when n & 2; rounding to float is sign-symmetric, so the
+     * sign goes onto the float (bit 1 of n into the sign bit).  sin(-0) must
+     * stay -0 (glibc returns y below 2^-12); the polynomial's fma(-0 * S1, -0)
+     * is +0.  Then sin/cos swap when n is odd: a bit-select on a mask of n & 1. */
+    const uint32_t fcb = qpsk_f32_bits((float)cp) ^ ((uint32_t)n << 30 & 0x80000000u);
+    const uint32_t fsb = y == 0.0f ? qpsk_f32_bits(y) : qpsk_f32_bits((float)sp);
+    const uint32_t odd = 0u - ((uint32_t)n & 1u);
+    union { uint32_t u; float f; } so, co;
+    so.u = (fcb & odd) | (fsb & ~odd);
+    co.u = (fsb & odd) | (fcb & ~odd);
+    *s = so.f;
+    *c = co.f;
 }
 #endif
