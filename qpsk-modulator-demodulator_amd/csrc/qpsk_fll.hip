@@ -59,18 +59,6 @@ struct FllSysLds {
     float taps[2 * kFllTaps];            // lower taps, reversed, interleaved (prologue)
 };
 
-// {x.x * v.x, x.x * v.y}
-__device__ __forceinline__ f2 mul_xlo(f2 x, f2 v) {
-    f2 r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "v"(x), "v"(v));
-    return r;
-}
-// {x.y * v.x, x.y * v.y}
-__device__ __forceinline__ f2 mul_xhi(f2 x, f2 v) {
-    f2 r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(r) : "v"(x), "v"(v));
-    return r;
-}
 // {p.x - q.y, p.y + q.x}
 __device__ __forceinline__ f2 add_swap_neglo(f2 p, f2 q) {
     f2 r;
@@ -218,6 +206,10 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
     partial(ring_at(0), 0);
 
     const float two_pi = 2.0f * 3.14159274101257324219f;
+    // the float sign bit in a VGPR for the sincos quadrant logic (v_bitop3_b32
+    // takes no literal): pinned once here, not rebuilt every sample
+    uint32_t sign_v = 0x80000000u;
+    asm volatile("" : "+v"(sign_v));
     const float beta = P.beta, alpha = P.alpha, fmax_ = P.max_freq, fmin_ = P.min_freq;
 
     // one sample (Band-Edge Filter.cs:102-129) at t = t0 + u, t0 a multiple of 8.
@@ -245,11 +237,13 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
 #endif
         } else {
             // a kept result has |phase| <= 2pi (or NaN): the branch-free form
-            qpsk_sincosf_glibc_fast(phase, &sn, &cs);
+            qpsk_sincosf_glibc_fast_k(phase, &sn, &cs, sign_v);
         }
-        const f2 csn = f2{cs, sn};
-        // (inI*c - inQ*s, inI*s + inQ*c)
-        const f2 xm = add_swap_neglo(mul_xlo(in, csn), mul_xhi(in, csn));
+        // (inI*c - inQ*s, inI*s + inQ*c) from p = in*c = {inI*c, inQ*c} and
+        // q = in*s = {inI*s, inQ*s}: {p.x - q.y, p.y + q.x}.  The broadcasts are
+        // op_sel_hi modifiers of one v_pk_mul_f32 each (plain vector code: no
+        // inline asm, whose hazards the compiler pads with s_nop)
+        const f2 xm = add_swap_neglo(in * f2{cs, cs}, in * f2{sn, sn});
         if constexpr (decltype(reg)::value) {
             xmv[u] = xm;
         } else {

@@ -130,18 +130,24 @@ QPSK_HDF static inline void qpsk_sincosf_glibc_small(float y, float *s, float *c
  * n = 0 and x = y exactly (y*2/pi*2^24 < 2^23, and fma(-0, pi/2, y) == y), and
  * below 2^-12 the polynomials round to y and 1 exactly (y = -0 aside, which is
  * kept by a select), so it returns what the branches return (tools/check_glibc_sincosf.c checks every such input). */
-QPSK_HDF static inline void qpsk_sincosf_glibc_fast(float y, float *s, float *c)
+/* The branch-free body.  SIGNV is 0x80000000; a device caller may pass it in a
+ * register it pinned once (asm "+v"), so the sign logic compiles to 3-input
+ * v_bitop3_b32 ops that cannot take a literal. */
+QPSK_HDF static inline void qpsk_sincosf_glibc_fast_k(float y, float *s, float *c, uint32_t SIGNV)
 {
     const double r = (double)y * 0x1.45F306DC9C883p+23;
     const int n = ((int32_t)r + 0x800000) >> 24;
     const double x = fma(-(double)n, 0x1.921FB54442D18p0, (double)y);
     const double x2 = x * x;
     /* The quadrant logic as bit operations on n (fewer instructions on the
-     * FLL's per-sample chain than compares and selects; the same bits):
-     * xs = -x when (n + 1) & 2 -- bit 1 of n + 1 moved into x's sign bit */
+     * FLL's per-sample chain than compares and selects; the same bits).
+     * t1 = n << 30 holds bit 1 of n in the sign position, t1 + 2^30 bit 1 of
+     * n + 1.  xs = -x when (n + 1) & 2: that bit XORed into x's sign */
+    const uint32_t t1 = (uint32_t)n << 30;
     union { double d; uint64_t u; } xb;
     xb.d = x;
-    xb.u ^= (uint64_t)(((uint32_t)n + 1u) << 30 & 0x80000000u) << 32;
+    const uint32_t xhi = (uint32_t)(xb.u >> 32) ^ ((t1 + 0x40000000u) & SIGNV);
+    xb.u = ((uint64_t)xhi << 32) | (uint32_t)xb.u;
     const double xs = xb.d;
     const double x3 = xs * x2;
     const double s1 = fma(x2, -0x1.994eb3774cf24p-13, 0x1.1107605230bc4p-7);
@@ -153,16 +159,31 @@ QPSK_HDF static inline void qpsk_sincosf_glibc_fast(float y, float *s, float *c)
     const double x6 = x4 * x2;
     const double cp = fma(x6, c2, fma(x4, 0x1.55553e1068f19p-5, c1));
     /* glibc negates cp when n & 2; rounding to float is sign-symmetric, so the
-     * sign goes onto the float (bit 1 of n into the sign bit).  sin(-0) must
+     * sign goes onto the float (bit 1 of n, i.e. t1's sign bit).  sin(-0) must
      * stay -0 (glibc returns y below 2^-12); the polynomial's fma(-0 * S1, -0)
-     * is +0.  Then sin/cos swap when n is odd: a bit-select on a mask of n & 1. */
-    const uint32_t fcb = qpsk_f32_bits((float)cp) ^ ((uint32_t)n << 30 & 0x80000000u);
+     * is +0.  Then sin/cos swap when n is odd: a bit-select on the mask
+     * -(n & 1) (a sign-extended bit-field extract on the device). */
+    const uint32_t fcb = qpsk_f32_bits((float)cp) ^ (t1 & SIGNV);
     const uint32_t fsb = y == 0.0f ? qpsk_f32_bits(y) : qpsk_f32_bits((float)sp);
-    const uint32_t odd = 0u - ((uint32_t)n & 1u);
     union { uint32_t u; float f; } so, co;
+#if defined(__HIP_DEVICE_COMPILE__)
+    /* one mask, two bit-field inserts (the compiler's own form of the select
+     * builds both -(n & 1) and its complement) */
+    uint32_t odd;
+    asm("v_bfe_i32 %2, %3, 0, 1\n\tv_bfi_b32 %0, %2, %4, %5\n\tv_bfi_b32 %1, %2, %5, %4"
+        : "=&v"(so.u), "=&v"(co.u), "=&v"(odd)
+        : "v"(n), "v"(fcb), "v"(fsb));
+#else
+    const uint32_t odd = 0u - ((uint32_t)n & 1u);
     so.u = (fcb & odd) | (fsb & ~odd);
     co.u = (fsb & odd) | (fcb & ~odd);
+#endif
     *s = so.f;
     *c = co.f;
+}
+
+QPSK_HDF static inline void qpsk_sincosf_glibc_fast(float y, float *s, float *c)
+{
+    qpsk_sincosf_glibc_fast_k(y, s, c, 0x80000000u);
 }
 #endif

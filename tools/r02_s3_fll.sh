@@ -9,7 +9,7 @@ for i in 1 2; do
   for lib in qpsk-modulator-demodulator_amd/_build/ab/lib*.so; do
     for mode in "" "--serial-calls"; do
       out=$(QPSK_DEMOD_LIB=$PWD/$lib timeout -k 10 300 python3 bench.py --timed-only --config c5 --steps 4 --warmup 1 $mode) || exit 1
-      echo "$(basename $lib) ${mode:-pipelined} $(echo "$out" | grep -o '"fll": [0-9.]*' | head -1) $(echo "$out" | grep -o '"loop": [0-9.]*' | head -1) $(echo "$out" | grep -o '"value": [0-9.]*' | head -1)"
+      echo "$(basename $lib) ${mode:-pipelined} $(echo "$out" | grep -o '"fll": [0-9][0-9.]*' | head -1) $(echo "$out" | grep -o '"loop": [0-9][0-9.]*' | head -1) $(echo "$out" | grep -o '"value": [0-9.]*' | head -1)"
     done
   done
 done
