@@ -80,6 +80,9 @@ constexpr int kCap128Sps2 = 72;
 // matched-filter workgroup of the next pipelined call fits beside it
 constexpr int kCapSps4 = 28;
 constexpr int kCapSps8 = 14;
+// 128-sample rounds at sps >= 8 (variant 4): lag_max = 64 needs
+// (CAP - 1)(sps - 0.1) >= KB + 4 + 64 -> CAP = 26
+constexpr int kCap128Sps8 = 26;
 typedef double d2 __attribute__((ext_vector_type(2)));
 
 // M&M -> Costas symbol slots: doubles (default; the M&M wave has them widened
@@ -842,6 +845,8 @@ void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant,
         launch_loop_spw<16, kCapSps2, 64>(a, P, mode, stream);
     else if (variant == 3)
         launch_loop_spw<16, kCap128Sps2, 128>(a, P, mode, stream);
+    else if (variant == 4 && P.sps >= 8.0)
+        launch_loop_spw<24, kCap128Sps8, 128>(a, P, mode, stream);
     else if (P.sps >= 8.0)
         launch_loop_spw<32, kCapSps8, 64>(a, P, mode, stream);
     else if (P.sps >= 4.0)

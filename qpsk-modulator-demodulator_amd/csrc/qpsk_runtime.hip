@@ -463,9 +463,9 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
         delete h;
         return fail(QPSK_ERR_ARGUMENT, "vector_lanes must be 1, 4, 8 or 16");
     }
-    if (p->loop_variant < 0 || p->loop_variant > 3) {
+    if (p->loop_variant < 0 || p->loop_variant > 4) {
         delete h;
-        return fail(QPSK_ERR_ARGUMENT, "loop_variant must be 0..3");
+        return fail(QPSK_ERR_ARGUMENT, "loop_variant must be 0..4");
     }
     std::string err;
     int rc = design_loops(p->sample_rate, p->symbol_rate, p->rrc_alpha, p->rrc_span,
@@ -512,6 +512,17 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
     };
     if (hipSetDevice(p->device) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipSetDevice failed (no GPU?)"));
+    // auto loop shape at sps >= 8: 24 streams x 128-sample rounds halve the
+    // per-round bookkeeping per symbol (C2 loop 23.9 -> 22.2-22.95 ms, A/B x3 on
+    // one MI355X) but take 147 KB of LDS, one workgroup per CU; above one
+    // workgroup per CU (C5: 8192 streams = 342 workgroups) the 32 x 64 shape
+    // (256 workgroups) is the faster one (C5 serial loop 24.0 vs 39.2 ms)
+    if (h->loop_variant == 0 && h->lp.sps >= 8.0) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) == hipSuccess &&
+            (h->S + 23) / 24 <= cus)
+            h->loop_variant = 4;
+    }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipStreamCreate failed"));
     h->own_stream = true;
