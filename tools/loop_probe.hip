@@ -36,7 +36,7 @@ __global__ void burn_kernel(float *sink, long long ticks) {
 int main(int argc, char** argv) {
   const int S = argc > 1 ? atoi(argv[1]) : 256;
   const int64_t n = argc > 2 ? atoll(argv[2]) : (1 << 20);
-  const int spw = argc > 3 ? atoi(argv[3]) : 0;   // loop_variant: 0 auto, 1 16x64, 2 32x64, 3 16x128
+  const int spw = argc > 3 ? atoi(argv[3]) : 0;   // loop_variant: 0 auto, 1 16x64, 2 32x64, 3 16x128, 4 24x128
   const int64_t stride = ((kMfPrefix + n + 2 + 63) / 64) * 64;
   // 32 distinct noise rows, replicated over the batch (host generation of a
   // C3-sized batch would take minutes)
@@ -89,7 +89,8 @@ int main(int argc, char** argv) {
   printf("S=%d n=%lld variant=%d burn=%d: %.3f ms, stream0 symbols %lld -> %.1f ns/symbol, WG0 M&M cycles %.3g -> %.2f GHz effective\n",
          S, (long long)n, spw, burn, ms, (long long)ns, ms * 1e6 / ns, (double)(pr[2] + pr[3]),
          (double)(pr[2] + pr[3]) / (ms * 1e6));
-  const int nwg = (int)((S + (spw == 0 || spw == 2 ? 32 : 16) - 1) / (spw == 0 || spw == 2 ? 32 : 16));
+  const int wgs = spw == 0 || spw == 2 ? 32 : (spw == 4 ? 24 : 16);
+  const int nwg = (S + wgs - 1) / wgs;
   for (int b = 0; b < nwg; ++b) {
     auto* p = &pr[16 * b];
     printf(" WG %2d:", b);
