@@ -51,6 +51,9 @@ FS = 10_000_000
 ALPHA = 0.4000000059604645            # (double)0.4f, testAtDataLevel.cs:18
 HBM_PEAK_GBS = 8000.0                 # MI355X_MICROARCH.md chip table (spec)
 FP32_PEAK_TFLOPS = 157.3              # MI355X_MICROARCH.md: peak FP32 vector (spec)
+# the reference rounds every product and every sum (no FMA), so a mul or an
+# add -- packed or not -- is one flop per lane-op: half the FMA peak
+FP32_PEAK_UNFUSED_TFLOPS = FP32_PEAK_TFLOPS / 2
 METRIC = "complex MSa/s through full demod chain (batched streams); BER vs CPU ref"
 
 CONFIGS = {
@@ -454,6 +457,8 @@ def rooflines(st, S, n, cfg):
                       "frac": round(gbs / HBM_PEAK_GBS, 4),
                       "valu_tflops": round(tfl, 2), "valu_peak_tflops": FP32_PEAK_TFLOPS,
                       "valu_frac": round(tfl / FP32_PEAK_TFLOPS, 4),
+                      "valu_peak_unfused_tflops": FP32_PEAK_UNFUSED_TFLOPS,
+                      "valu_frac_unfused": round(tfl / FP32_PEAK_UNFUSED_TFLOPS, 4),
                       "per_unit": f"16 B and {4 * T} flop per complex sample, {S * n} samples per launch"}
     if st["loop"] > 0:
         loop_s = st["loop"] / 1e3
@@ -584,6 +589,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
         r = rl[dom]
         roof = {"bound": r["bound"], "kernel": r["kernel"], "achieved": r["achieved"], "peak": r["peak"],
                 "unit": r["unit"], "frac": r["frac"], "valu_frac": r.get("valu_frac"),
+                "valu_frac_unfused": r.get("valu_frac_unfused"),
                 "traffic": (load_traffic(key) if dom == "fir" and S == cfg["streams"] and n == 1 << 20
                             else None)}
     rec = {
