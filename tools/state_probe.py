@@ -1,8 +1,7 @@
 """Diagnostic: per-call loop-kernel time and loop-state statistics over a
 sustained run of consecutive DeModulate calls on the same synthetic batch.
 
-Reports, after each call, how many streams have |theta| > 1e6 (the Costas
-fast sincos' range), |freq| > pi (the single +-2pi wrap can
+Reports, after each call, how many streams have |theta| > 1e6 (round 1's Costas fast-sincos range) and > 2^40 (the current range), |freq| > pi (the single +-2pi wrap can
 no longer bound theta), a non-finite M&M time, or a sticky error flag."""
 import argparse
 import json
@@ -57,8 +56,9 @@ def main():
         d.enable_timing(False)
         s = np.frombuffer(d.get_state()[: S * STATE.itemsize], dtype=STATE)
         th, fr = np.abs(s["theta"]), np.abs(s["freq"])
-        rec = {"call": c, "fir_ms": round(t["fir"], 2), "loop_ms": round(t["loop"], 2),
-               "theta_gt_1e6": int((th > 1e6).sum()), "theta_max": float(th.max()),
+        rec = {"call": c, "fll_ms": round(t.get("fll", 0.0), 2), "fir_ms": round(t["fir"], 2), "loop_ms": round(t["loop"], 2),
+               "theta_gt_1e6": int((th > 1e6).sum()), "theta_gt_2p40": int((th > 2.0 ** 40).sum()),
+               "theta_max": float(th.max()),
                "freq_gt_pi": int((fr > np.pi).sum()), "freq_max": float(fr.max()),
                "mu_nonfinite": int((~np.isfinite(s["mu"])).sum()),
                "error_flags": int((s["error"] != 0).sum()),
