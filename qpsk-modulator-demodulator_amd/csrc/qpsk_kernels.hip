@@ -150,16 +150,15 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, TapsRev taps, c
 #pragma unroll
         for (int q = 0; q < Q; ++q) acc[q] = f2{0.f, 0.f};
     }
-#pragma unroll
-    for (int l = 0; l < W && J > 0; ++l) {
+    // Lane accumulator l of every output: sum_j hrev[jW+l] * x[t-T+1+jW+l],
+    // j ascending (FIRFilter.cs:165-174); u_i = x[t0 + l + W i] is shared by
+    // the Q outputs of this thread.  RD(i) reads u_i.
+    auto lane_phase = [&](int l, auto rdu) __attribute__((always_inline)) {
         if constexpr (kPhasedTaps) asm volatile("" ::: "memory");
-        // Lane accumulator l of every output: sum_j hrev[jW+l] * x[t-T+1+jW+l],
-        // j ascending (FIRFilter.cs:165-174); u_i = x[t0 + l + W i] is shared by
-        // the Q outputs of this thread.
         f2 A[Q];
 #pragma unroll
         for (int i = 0; i < Q + J - 1; ++i) {
-            const f2 u = rd(l + W * i);
+            const f2 u = rdu(i);
             f2 p[Q];   // all products of u first, then the adds (no mul->add stall)
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
@@ -175,6 +174,26 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, TapsRev taps, c
         // Horizontal sum in lane order 0..W-1 (FIRFilter.cs:176-180).
 #pragma unroll
         for (int q = 0; q < Q; ++q) acc[q] = (l == 0) ? A[q] : acc[q] + A[q];
+    };
+    if constexpr (J > 0 && W == 8) {
+        // lane phase 0 unrolled, phases 1..7 as one rolled body: 6.8 KB of code
+        // at T = 129 instead of 20.9 KB, and 2 % faster (C3 FIR alone 41.2 ->
+        // 40.4 ms, A/B x2, profiles/r02_fir_roll_ab.txt).  With l at run time,
+        // input l + 8i sits at row + l + 8i + 8(i/8), plus 8 more when
+        // r + l + 8(i%8) >= 64, i.e. i%8 == 7 and r + l >= 8
+        lane_phase(0, [&](int i) { return rd(W * i); });
+#pragma unroll 1
+        for (int l = 1; l < W; ++l) {
+            const f2 *rowl = row + l;
+            const f2 *rowlw = rowl + ((r + l) >= 8 ? 8 : 0);
+            lane_phase(l, [&](int i) {
+                const int off = 8 * i + 8 * (i >> 3);
+                return (i & 7) == 7 ? rowlw[off] : rowl[off];
+            });
+        }
+    } else {
+#pragma unroll
+        for (int l = 0; l < W && J > 0; ++l) lane_phase(l, [&](int i) { return rd(l + W * i); });
     }
 #pragma unroll
     for (int k = 0; k < TAIL; ++k) {
