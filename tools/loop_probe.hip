@@ -100,7 +100,8 @@ int main(int argc, char** argv) {
     }
     printf(" M&M %.0f Costas %.0f cyc/sym\n", (double)p[3] / (p[4] & 0xfffff), (double)p[6] / (p[4] & 0xfffff));
   }
-  for (int b = 0; b < 3; ++b) {
+  for (int bi = 0; bi < 3; ++bi) {
+    const int b = bi < 2 ? bi : nwg - 1;   // the first two and the last (maybe partial) workgroup
     auto* p = &pr[16 * b];
     const double R = (double)p[7];
     printf(" WG %d rounds %llu: per round cycles: loader wait %.0f bar %.0f issue %.0f | M&M bar %.0f loop %.0f | Costas bar %.0f loop %.0f | cyc/sym M&M %.0f Costas %.0f | M&M uniform-loop cycles/round %.0f (%.0f/sym) | Costas uniform %.0f/round (%.0f/sym) | M&M pre %.0f post %.0f\n",
