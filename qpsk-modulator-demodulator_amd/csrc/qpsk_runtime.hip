@@ -516,11 +516,14 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
     // per-round bookkeeping per symbol (C2 loop 23.9 -> 22.2-22.95 ms, A/B x3 on
     // one MI355X) but take 147 KB of LDS, one workgroup per CU; above one
     // workgroup per CU (C5: 8192 streams = 342 workgroups) the 32 x 64 shape
-    // (256 workgroups) is the faster one (C5 serial loop 24.0 vs 39.2 ms)
+    // (256 workgroups) is the faster one (C5 serial loop 24.0 vs 39.2 ms).
+    // Above half the CUs, too: no FIR workgroup fits beside a 147 KB one, and
+    // pipelined calls then wait for the FIR (4096 streams: 37.7 vs 33.4 ms a
+    // call; 2048: 24.6 vs 29.1 ms, profiles/r02_loop_shapes_c4_ab.txt)
     if (h->loop_variant == 0 && h->lp.sps >= 8.0) {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) == hipSuccess &&
-            (h->S + 23) / 24 <= cus)
+            (h->S + 23) / 24 <= cus / 2)
             h->loop_variant = 4;
     }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
