@@ -167,13 +167,20 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     const int blk_s0 = static_cast<int>(static_cast<int64_t>(blockIdx.x) * a.S / gridDim.x);
     const int nvalid = static_cast<int>(static_cast<int64_t>(blockIdx.x + 1) * a.S / gridDim.x) - blk_s0;
     const int s = blk_s0 + lane;
-    const bool valid = lane < nvalid;
+    // lanes SPW > l >= nvalid shadow the workgroup's first stream: they run its
+    // M&M and Costas chains too (on the copy of its samples the loader puts in
+    // their ring rows) and write nothing.  A wave with 16 or fewer active lanes
+    // runs these loops 10-50 % slower per symbol than one with 20 or more
+    // (profiles/r02_loop_probe_lanes.txt), so small batches keep SPW lanes busy
+    const bool real = lane < nvalid;            // owns stream s: writes its results
+    const bool valid = lane < SPW;              // computes stream sc
+    const int sc = real ? s : blk_s0;
 
-    // ---- per-stream queue geometry (every wave: lane l <-> stream blk*SPW + l)
+    // ---- per-stream queue geometry (every wave: lane l <-> stream sc)
     int n = 0, cnt = 0, R = 0, d = 0;
     if (valid) {
-        n = static_cast<int>(a.lengths ? a.lengths[s] : a.n);
-        R = a.state[s].carry_n;
+        n = static_cast<int>(a.lengths ? a.lengths[sc] : a.n);
+        R = a.state[sc].carry_n;
         d = R & 1;
         cnt = R + d + n;
         // DeModulate with an empty span returns before touching any state (:350-351)
@@ -198,7 +205,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     if (wave == 0) {
         // ============================================================ loader
         // one glds instruction = KB/2 lanes x 16 B = one stream's round (8*KB bytes)
-        const int64_t org = valid ? s * a.mf_stride + kMfPrefix - R - d : 0;
+        const int64_t org = valid ? sc * a.mf_stride + kMfPrefix - R - d : 0;
         const int c2 = 2 * (lane % (KB / 2));
         const f2 *mf = reinterpret_cast<const f2 *>(a.mf);
         const bool lo_half = lane < KB / 2;
@@ -293,7 +300,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     if (wave == 1) {
         // ============================================================ M&M
         StreamState st;
-        if (mine) st = a.state[s];
+        if (mine) st = a.state[sc];
         int base = mine ? st.base + d : 0;          // physical baseIndex
         double mu = st.mu, integ = st.integ;
         float psi = st.psi, psq = st.psq, pdi = st.pdi, pdq = st.pdq;
@@ -547,7 +554,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             a.probe[blockIdx.x * 16 + 11] = c_pre + (c_post << 32);
         }
 #endif
-        if (!valid) return;
+        if (!real) return;
         if (!mine) {   // empty DeModulate call: nothing changes
             if (a.n_syms) a.n_syms[s] = 0;
             return;
@@ -609,8 +616,8 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         // ============================================================ Costas
         double theta = 0.0, freq = 0.0;
         if (mine) {
-            theta = a.state[s].theta;
-            freq = a.state[s].freq;
+            theta = a.state[sc].theta;
+            freq = a.state[sc].freq;
         }
         double ca = P.c_alpha, cb = P.c_beta;
         double kTwoPi = 2.0 * 3.14159265358979311600;
@@ -724,7 +731,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             a.probe[blockIdx.x * 16 + 9] = k_uit;
         }
 #endif
-        if (mine) {
+        if (real && mine) {
             a.state[s].theta = theta;
             a.state[s].freq = freq;
         }
@@ -736,15 +743,17 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     for (int r = 0; r <= NR + 1; ++r) __builtin_amdgcn_s_barrier();   // diagnostic
     return;
 #endif
+    // the decode wave runs the real lanes only (its per-lane loop is off the chains)
+    const bool dmine = real && mine;
     int diff_have = 0;
     float dpi = 0.f, dpq = 0.f;
-    if (mine) {
+    if (dmine) {
         diff_have = a.state[s].diff_have;
         dpi = a.state[s].diff_pi;
         dpq = a.state[s].diff_pq;
     }
-    uint32_t *bits = (MODE == kModeDemodulate && mine) ? a.bits + s * a.bits_stride_words : nullptr;
-    f2 *syms = (SYMS && mine) ? reinterpret_cast<f2 *>(a.syms) + s * a.syms_stride : nullptr;
+    uint32_t *bits = (MODE == kModeDemodulate && dmine) ? a.bits + s * a.bits_stride_words : nullptr;
+    f2 *syms = (SYMS && dmine) ? reinterpret_cast<f2 *>(a.syms) + s * a.syms_stride : nullptr;
     uint32_t word = 0;
     int wbits = 0;
     int64_t widx = 0, nbits = 0, ncs = 0;
@@ -753,7 +762,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         __builtin_amdgcn_s_barrier();
         if (r < 2) continue;
         const int slot = (r - 2) & 1;
-        const int m = mine ? L.cnt[((r - 2) & 3) * SPW + lane] : 0;
+        const int m = dmine ? L.cnt[((r - 2) & 3) * SPW + lane] : 0;
         const f2 *in = L.rot + (slot * SPW + lane) * L.RS;
         for (int k = 0; k < m; ++k) {
             const f2 rr = in[k];
@@ -795,7 +804,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             }
         }
     }
-    if (!valid) return;
+    if (!real) return;
     if (!mine) {
         if (a.n_bits) a.n_bits[s] = 0;
         return;
