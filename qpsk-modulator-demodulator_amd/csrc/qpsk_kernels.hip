@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "qpsk_kernels.h"
 #include "qpsk_sincos.h"
@@ -77,75 +78,31 @@ __device__ __forceinline__ f2 fir_exact_one(XF x, const float *hrev, int T, int 
     return f2{ai, aq};
 }
 
-template <int T, int W, int Q, bool VEC, int NT>
-__global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, TapsRev taps, const float *hrev) {
-    constexpr int TILE = NT * Q;
-    constexpr int NIN = TILE + T - 1;
+// The arithmetic of Q outputs of one thread: row = the thread's LDS row base
+// (lds + 72 * grp + r), outputs t0 + W*q, q < Q, t0 = 64*grp + r.  A group of
+// W threads covers one 64-sample LDS row of outputs.  The read of input t0 + c
+// (c a compile-time offset) lands in slot 72*grp + r + c + 8*floor((r+c)/64);
+// the floor is compile-time except when c mod 64 > 56, so almost every ds_read
+// uses an immediate offset and the 8-slot row pad keeps the four groups of a
+// half-wave on distinct banks.
+template <int T, int W, int Q>
+__device__ __forceinline__ void fir_core(const f2 *row, int r, const float *hrev, f2 (&acc)[Q]) {
     constexpr int J = T / W;          // full Vector<float> blocks
     constexpr int NVEC = J * W;
     constexpr int TAIL = T - NVEC;    // scalar tail taps (FIRFilter.cs:183-192)
-    __shared__ f2 lds[lds_slots(NIN)];
-
-    const int s = blockIdx.y;
-    const int64_t tile0 = static_cast<int64_t>(blockIdx.x) * TILE;
-    const int64_t n = a.lengths ? a.lengths[s] : a.n;
-    if (tile0 >= n) return;
-    const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
-    const f2 *hist = reinterpret_cast<const f2 *>(a.hist) + static_cast<int64_t>(s) * (T - 1);
-    const int tid = threadIdx.x;
-
-    // Stage x[tile0-(T-1) .. tile0+TILE) ; t<0 from the previous call's history,
-    // t>=n as zeros (those outputs are not stored).
-    const int64_t g0 = tile0 - (T - 1);
-    if constexpr (VEC) {
-        // g0 is even (T odd) and rows are 16-B aligned: one float4 = 2 samples.
-        for (int p = tid; p < (NIN + 1) / 2; p += NT) {
-            const int64_t g = g0 + 2 * p;
-            f4 v;
-            if (g >= 0 && g + 1 < n) {
-                v = *reinterpret_cast<const f4 *>(x + g);
-            } else {
-                f2 lo = g < 0 ? hist[T - 1 + g] : (g < n ? x[g] : f2{0.f, 0.f});
-                f2 hi = (g + 1) < 0 ? hist[T + g] : ((g + 1) < n ? x[g + 1] : f2{0.f, 0.f});
-                v = f4{lo.x, lo.y, hi.x, hi.y};
-            }
-            *reinterpret_cast<f4 *>(&lds[lds_slot(2 * p)]) = v;
-        }
-    } else {
-        for (int i = tid; i < NIN; i += NT) {
-            const int64_t g = g0 + i;
-            lds[lds_slot(i)] = g < 0 ? hist[T - 1 + g] : (g < n ? x[g] : f2{0.f, 0.f});
-        }
-    }
-    __syncthreads();
-
-    // Thread -> outputs t0 + W*q, q < Q, t0 = 64*grp + r: a group of W threads
-    // covers one 64-sample LDS row of outputs.  The read of input t0 + c (c a
-    // compile-time offset) lands in slot 72*grp + r + c + 8*floor((r+c)/64);
-    // the floor is compile-time except when c mod 64 > 56, so almost every
-    // ds_read uses an immediate offset and the 8-slot row pad keeps the four
-    // groups of a half-wave on distinct banks.
     static_assert(W * Q == 64, "specialised FIR expects W*Q == 64");
-    const int grp = tid / W, r = tid % W;
-    const f2 *row = lds + 72 * grp + r;
     auto rd = [&](int c) -> f2 {
         const int lo = c >> 6, hi = (c + W - 1) >> 6;
         if (lo == hi) return row[c + 8 * lo];
         return row[c + 8 * lo + ((r + (c & 63)) >= 64 ? 8 : 0)];
     };
-    // Long filters (T > 80): the taps no longer fit in SGPRs next to everything
-    // else and hipcc spills them through v_writelane/v_readlane (+26 % VALU at
-    // T = 129).  Instead each lane phase l loads only its own J taps (uniform
-    // loads from the device copy) after a compiler barrier, so at most J taps
-    // are live at a time.
-    constexpr bool kPhasedTaps = true;
+    // Taps are uniform scalar loads from the device copy, issued per lane phase
+    // l behind a compiler barrier, so at most J taps are live at a time (long
+    // filters would otherwise spill SGPR taps through v_writelane/v_readlane:
+    // +26 % VALU at T = 129).
     typedef __attribute__((address_space(4))) const float cfloat;   // scalar (s_load) path
     cfloat *hc = (cfloat *)hrev;
-    auto tap = [&](int idx) -> float {
-        if constexpr (kPhasedTaps) return hc[idx];
-        else return taps.h[idx];
-    };
-    f2 acc[Q];
+    auto tap = [&](int idx) -> float { return hc[idx]; };
     if constexpr (J == 0) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) acc[q] = f2{0.f, 0.f};
@@ -154,7 +111,7 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, TapsRev taps, c
     // j ascending (FIRFilter.cs:165-174); u_i = x[t0 + l + W i] is shared by
     // the Q outputs of this thread.  RD(i) reads u_i.
     auto lane_phase = [&](int l, auto rdu) __attribute__((always_inline)) {
-        if constexpr (kPhasedTaps) asm volatile("" ::: "memory");
+        asm volatile("" ::: "memory");
         f2 A[Q];
 #pragma unroll
         for (int i = 0; i < Q + J - 1; ++i) {
@@ -203,6 +160,58 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, TapsRev taps, c
             acc[q] = acc[q] + tap(NVEC + k) * u;
         }
     }
+}
+
+__device__ __forceinline__ int fir_nonfinite(float v) { return __builtin_amdgcn_classf(v, 0x207); }   // NaN, +-Inf
+
+// Stage x[tile0-(T-1) .. tile0+TILE) into LDS; t<0 from the previous call's
+// history, t>=n as zeros (those outputs are not stored).
+template <int T, int NIN, bool VEC, int NT>
+__device__ __forceinline__ void fir_stage(f2 *lds, const f2 *x, const f2 *hist, int64_t tile0, int64_t n) {
+    const int tid = threadIdx.x;
+    const int64_t g0 = tile0 - (T - 1);
+    if constexpr (VEC) {
+        // g0 is even (T odd) and rows are 16-B aligned: one float4 = 2 samples.
+        for (int p = tid; p < (NIN + 1) / 2; p += NT) {
+            const int64_t g = g0 + 2 * p;
+            f4 v;
+            if (g >= 0 && g + 1 < n) {
+                v = *reinterpret_cast<const f4 *>(x + g);
+            } else {
+                f2 lo = g < 0 ? hist[T - 1 + g] : (g < n ? x[g] : f2{0.f, 0.f});
+                f2 hi = (g + 1) < 0 ? hist[T + g] : ((g + 1) < n ? x[g + 1] : f2{0.f, 0.f});
+                v = f4{lo.x, lo.y, hi.x, hi.y};
+            }
+            *reinterpret_cast<f4 *>(&lds[lds_slot(2 * p)]) = v;
+        }
+    } else {
+        for (int i = tid; i < NIN; i += NT) {
+            const int64_t g = g0 + i;
+            lds[lds_slot(i)] = g < 0 ? hist[T - 1 + g] : (g < n ? x[g] : f2{0.f, 0.f});
+        }
+    }
+}
+
+template <int T, int W, int Q, bool VEC, int NT>
+__global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, TapsRev taps, const float *hrev) {
+    constexpr int TILE = NT * Q;
+    constexpr int NIN = TILE + T - 1;
+    __shared__ f2 lds[lds_slots(NIN)];
+
+    const int s = blockIdx.y;
+    const int64_t tile0 = static_cast<int64_t>(blockIdx.x) * TILE;
+    const int64_t n = a.lengths ? a.lengths[s] : a.n;
+    if (tile0 >= n) return;
+    const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
+    const f2 *hist = reinterpret_cast<const f2 *>(a.hist) + static_cast<int64_t>(s) * (T - 1);
+    const int tid = threadIdx.x;
+
+    fir_stage<T, NIN, VEC, NT>(lds, x, hist, tile0, n);
+    __syncthreads();
+
+    const int grp = tid / W, r = tid % W;
+    f2 acc[Q];
+    fir_core<T, W, Q>(lds + 72 * grp + r, r, hrev, acc);
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < Q; ++q) lds[72 * grp + r + W * q] = acc[q];
@@ -212,13 +221,12 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, TapsRev taps, c
     // fast output non-finite; the stores below watch for that, and such a tile
     // is recomputed with the reference's full products straight from HBM.
     int bad = 0;
-    auto nonfinite = [](float v) -> int { return __builtin_amdgcn_classf(v, 0x207); };   // NaN, +-Inf
     f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride + a.y_offset;
     if constexpr (VEC) {
         for (int p = tid; p < TILE / 2; p += NT) {
             const int64_t g = tile0 + 2 * p;
             const f4 v = *reinterpret_cast<const f4 *>(&lds[lds_slot(2 * p)]);
-            bad |= nonfinite(v.x) | nonfinite(v.y) | nonfinite(v.z) | nonfinite(v.w);
+            bad |= fir_nonfinite(v.x) | fir_nonfinite(v.y) | fir_nonfinite(v.z) | fir_nonfinite(v.w);
             if (g + 1 < n) {
                 *reinterpret_cast<f4 *>(y + g) = v;
             } else if (g < n) {
@@ -229,7 +237,7 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, TapsRev taps, c
         for (int i = tid; i < TILE; i += NT) {
             const int64_t g = tile0 + i;
             const f2 v = lds[lds_slot(i)];
-            bad |= nonfinite(v.x) | nonfinite(v.y);
+            bad |= fir_nonfinite(v.x) | fir_nonfinite(v.y);
             if (g < n) y[g] = v;
         }
     }
@@ -245,6 +253,69 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, TapsRev taps, c
                 return g < 0 ? hist[T - 1 + g] : x[g];
             };
             y[go] = fir_exact_one(xs, hrev, T, W);
+        }
+    }
+}
+
+// Work-sharing variant: a tile of U units of 512 outputs (one wave's Q = 8
+// outputs per lane), staged once by the workgroup; then every wave takes
+// units from an LDS counter until none is left and stores its outputs
+// straight from registers.  Beside the loop kernel a workgroup's waves sit on
+// SIMDs with very different loads (the M&M and Costas waves are VALU-heavy,
+// the loader and decode waves light); with one unit per wave the workgroup
+// runs at its slowest wave's pace, here the waves on the light SIMDs take
+// more units.  Same arithmetic (fir_core), same outputs.
+template <int T, int U, int NT, bool VEC>
+__global__ __launch_bounds__(NT) void fir_share_kernel(FirArgs a, const float *hrev) {
+    constexpr int W = 8, Q = 8;
+    constexpr int UNIT = 64 * Q;
+    constexpr int TILE = U * UNIT;
+    constexpr int NIN = TILE + T - 1;
+    __shared__ f2 lds[lds_slots(NIN)];
+    __shared__ int next_unit;
+
+    const int s = blockIdx.y;
+    const int64_t tile0 = static_cast<int64_t>(blockIdx.x) * TILE;
+    const int64_t n = a.lengths ? a.lengths[s] : a.n;
+    if (tile0 >= n) return;
+    const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
+    const f2 *hist = reinterpret_cast<const f2 *>(a.hist) + static_cast<int64_t>(s) * (T - 1);
+    if (threadIdx.x == 0) next_unit = 0;
+    fir_stage<T, NIN, VEC, NT>(lds, x, hist, tile0, n);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int grp = lane / W, r = lane % W;
+    const int64_t rem = n - tile0;
+    const int nunits = rem >= TILE ? U : static_cast<int>((rem + UNIT - 1) / UNIT);
+    f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride + a.y_offset;
+    for (;;) {
+        int u = 0;
+        if (lane == 0) u = atomicAdd(&next_unit, 1);
+        u = __builtin_amdgcn_readfirstlane(u);
+        if (u >= nunits) break;
+        f2 acc[Q];
+        fir_core<T, W, Q>(lds + 72 * (8 * u + grp) + r, r, hrev, acc);
+        const int64_t o0 = tile0 + static_cast<int64_t>(u) * UNIT + 64 * grp + r;
+        int bad = 0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int64_t g = o0 + W * q;
+            bad |= fir_nonfinite(acc[q].x) | fir_nonfinite(acc[q].y);
+            if (g < n) y[g] = acc[q];
+        }
+        if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {   // rare: the reference's full products
+#pragma unroll 1
+            for (int q = 0; q < Q; ++q) {
+                const int64_t go = o0 + W * q;
+                if (go >= n) continue;
+                const int64_t w0 = go - (T - 1);
+                auto xs = [&](int k) -> f2 {
+                    const int64_t g = w0 + k;
+                    return g < 0 ? hist[T - 1 + g] : x[g];
+                };
+                y[go] = fir_exact_one(xs, hrev, T, W);
+            }
         }
     }
 }
@@ -465,9 +536,38 @@ static void launch_fir_w8_nt(const FirArgs &a, const TapsRev &taps, const float 
         hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, false, NT>), grid, dim3(NT), 0, stream, a, taps, hrev);
 }
 
+template <int T, int U, int NT>
+static void launch_fir_share(const FirArgs &a, const float *hrev, int S, int64_t n_max, bool vec,
+                             hipStream_t stream) {
+    const int64_t tiles = (n_max + U * 512 - 1) / (U * 512);
+    dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(S));
+    if (vec)
+        hipLaunchKernelGGL((fir_share_kernel<T, U, NT, true>), grid, dim3(NT), 0, stream, a, hrev);
+    else
+        hipLaunchKernelGGL((fir_share_kernel<T, U, NT, false>), grid, dim3(NT), 0, stream, a, hrev);
+}
+
+// experiment switch (QPSK_FIR_SHARE = units*1000 + threads, e.g. 6256); 0 = tile kernel
+static int fir_share_mode() {
+    static int mode = -1;
+    if (mode < 0) {
+        const char *e = getenv("QPSK_FIR_SHARE");
+        mode = e ? atoi(e) : 0;
+    }
+    return mode;
+}
+
 template <int T>
 static bool launch_fir_w8(const FirArgs &a, const TapsRev &taps, const float *hrev, int S,
                           int64_t n_max, bool vec, hipStream_t stream) {
+    switch (fir_share_mode()) {
+    case 4256: launch_fir_share<T, 4, 256>(a, hrev, S, n_max, vec, stream); return true;
+    case 6256: launch_fir_share<T, 6, 256>(a, hrev, S, n_max, vec, stream); return true;
+    case 8256: launch_fir_share<T, 8, 256>(a, hrev, S, n_max, vec, stream); return true;
+    case 4128: launch_fir_share<T, 4, 128>(a, hrev, S, n_max, vec, stream); return true;
+    case 3128: launch_fir_share<T, 3, 128>(a, hrev, S, n_max, vec, stream); return true;
+    default: break;
+    }
     // 2048-output tiles; 1024- and 512-output tiles (128 / 64 threads, more
     // workgroups beside the loop kernel's) measured the same at C3 and C2
     // (pipelined bench, A/B x2 on one MI355X)
