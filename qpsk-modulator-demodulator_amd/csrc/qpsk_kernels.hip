@@ -22,7 +22,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <cstdlib>
 
 #include "qpsk_kernels.h"
 #include "qpsk_sincos.h"
@@ -257,69 +256,6 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, TapsRev taps, c
     }
 }
 
-// Work-sharing variant: a tile of U units of 512 outputs (one wave's Q = 8
-// outputs per lane), staged once by the workgroup; then every wave takes
-// units from an LDS counter until none is left and stores its outputs
-// straight from registers.  Beside the loop kernel a workgroup's waves sit on
-// SIMDs with very different loads (the M&M and Costas waves are VALU-heavy,
-// the loader and decode waves light); with one unit per wave the workgroup
-// runs at its slowest wave's pace, here the waves on the light SIMDs take
-// more units.  Same arithmetic (fir_core), same outputs.
-template <int T, int U, int NT, bool VEC>
-__global__ __launch_bounds__(NT) void fir_share_kernel(FirArgs a, const float *hrev) {
-    constexpr int W = 8, Q = 8;
-    constexpr int UNIT = 64 * Q;
-    constexpr int TILE = U * UNIT;
-    constexpr int NIN = TILE + T - 1;
-    __shared__ f2 lds[lds_slots(NIN)];
-    __shared__ int next_unit;
-
-    const int s = blockIdx.y;
-    const int64_t tile0 = static_cast<int64_t>(blockIdx.x) * TILE;
-    const int64_t n = a.lengths ? a.lengths[s] : a.n;
-    if (tile0 >= n) return;
-    const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
-    const f2 *hist = reinterpret_cast<const f2 *>(a.hist) + static_cast<int64_t>(s) * (T - 1);
-    if (threadIdx.x == 0) next_unit = 0;
-    fir_stage<T, NIN, VEC, NT>(lds, x, hist, tile0, n);
-    __syncthreads();
-
-    const int lane = threadIdx.x & 63;
-    const int grp = lane / W, r = lane % W;
-    const int64_t rem = n - tile0;
-    const int nunits = rem >= TILE ? U : static_cast<int>((rem + UNIT - 1) / UNIT);
-    f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride + a.y_offset;
-    for (;;) {
-        int u = 0;
-        if (lane == 0) u = atomicAdd(&next_unit, 1);
-        u = __builtin_amdgcn_readfirstlane(u);
-        if (u >= nunits) break;
-        f2 acc[Q];
-        fir_core<T, W, Q>(lds + 72 * (8 * u + grp) + r, r, hrev, acc);
-        const int64_t o0 = tile0 + static_cast<int64_t>(u) * UNIT + 64 * grp + r;
-        int bad = 0;
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int64_t g = o0 + W * q;
-            bad |= fir_nonfinite(acc[q].x) | fir_nonfinite(acc[q].y);
-            if (g < n) y[g] = acc[q];
-        }
-        if (__builtin_amdgcn_ballot_w64(bad != 0) != 0) {   // rare: the reference's full products
-#pragma unroll 1
-            for (int q = 0; q < Q; ++q) {
-                const int64_t go = o0 + W * q;
-                if (go >= n) continue;
-                const int64_t w0 = go - (T - 1);
-                auto xs = [&](int k) -> f2 {
-                    const int64_t g = w0 + k;
-                    return g < 0 ? hist[T - 1 + g] : x[g];
-                };
-                y[go] = fir_exact_one(xs, hrev, T, W);
-            }
-        }
-    }
-}
-
 // Any (T, W) without a specialised tile kernel: the reference's formula
 // itself, full complex products included (not on the benchmarked path).
 __global__ __launch_bounds__(256) void fir_generic_kernel(FirArgs a, const float *hrev, int T,
@@ -536,41 +472,14 @@ static void launch_fir_w8_nt(const FirArgs &a, const TapsRev &taps, const float 
         hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, false, NT>), grid, dim3(NT), 0, stream, a, taps, hrev);
 }
 
-template <int T, int U, int NT>
-static void launch_fir_share(const FirArgs &a, const float *hrev, int S, int64_t n_max, bool vec,
-                             hipStream_t stream) {
-    const int64_t tiles = (n_max + U * 512 - 1) / (U * 512);
-    dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(S));
-    if (vec)
-        hipLaunchKernelGGL((fir_share_kernel<T, U, NT, true>), grid, dim3(NT), 0, stream, a, hrev);
-    else
-        hipLaunchKernelGGL((fir_share_kernel<T, U, NT, false>), grid, dim3(NT), 0, stream, a, hrev);
-}
-
-// experiment switch (QPSK_FIR_SHARE = units*1000 + threads, e.g. 6256); 0 = tile kernel
-static int fir_share_mode() {
-    static int mode = -1;
-    if (mode < 0) {
-        const char *e = getenv("QPSK_FIR_SHARE");
-        mode = e ? atoi(e) : 0;
-    }
-    return mode;
-}
-
 template <int T>
 static bool launch_fir_w8(const FirArgs &a, const TapsRev &taps, const float *hrev, int S,
                           int64_t n_max, bool vec, hipStream_t stream) {
-    switch (fir_share_mode()) {
-    case 4256: launch_fir_share<T, 4, 256>(a, hrev, S, n_max, vec, stream); return true;
-    case 6256: launch_fir_share<T, 6, 256>(a, hrev, S, n_max, vec, stream); return true;
-    case 8256: launch_fir_share<T, 8, 256>(a, hrev, S, n_max, vec, stream); return true;
-    case 4128: launch_fir_share<T, 4, 128>(a, hrev, S, n_max, vec, stream); return true;
-    case 3128: launch_fir_share<T, 3, 128>(a, hrev, S, n_max, vec, stream); return true;
-    default: break;
-    }
     // 2048-output tiles; 1024- and 512-output tiles (128 / 64 threads, more
     // workgroups beside the loop kernel's) measured the same at C3 and C2
-    // (pipelined bench, A/B x2 on one MI355X)
+    // (pipelined bench, A/B x2 on one MI355X), and so did a
+    // work-sharing tile whose waves take 512-output units from an LDS counter
+    // (profiles/r02_fir_share_ab.txt)
     launch_fir_w8_nt<T, kFirThreads>(a, taps, hrev, S, n_max, vec, stream);
     return true;
 }
