@@ -356,6 +356,30 @@ def test_huge_amplitude_takes_the_costas_rollback_path():
     # theta leaves [-1e6, 1e6] within a round)
 
 
+@pytest.mark.parametrize("sps,span", [(8, 8), (4, 32)])
+def test_degenerate_streams_bit_exact(sps, span):
+    """Streams the synthetic batches never hold, beside normal ones, against
+    the oracle bit for bit: all zeros (every decision at +0, the TED and phase
+    error exactly 0), a signal scaled into the subnormal range (products and
+    interpolations below 2^-126: the kernels must not flush them), a constant
+    DC level, and a signal with a zeroed gap spanning calls."""
+    iq = K.batch_signals(6, seed0=700, sps=sps, span=span, n_bits=1200, snr_db=18)
+    iq[1] = 0.0
+    iq[2] = iq[2] * np.float32(1e-39)
+    assert np.count_nonzero(np.abs(iq[2]) < np.float32(2.0 ** -126)) > iq.shape[1] // 2
+    iq[3] = np.float32(0.25)
+    n = iq.shape[1] // 2
+    iq[4, 2 * (n // 3): 2 * (n // 3 + 700)] = 0.0
+    calls = [[n // 3 + 100] * 6, [0, 5, 17, 1, 300, 2], [n - n // 3 - 100, n - n // 3 - 105,
+                                                        n - n // 3 - 117, n - n // 3 - 101,
+                                                        n - n // 3 - 400, n - n // 3 - 102]]
+    got, ref = gpu_run(iq, calls, sps, span), oracle_run(iq, calls, sps, span)
+    for ci, (ra, rb) in enumerate(zip(got, ref)):
+        for s, ((ba, sa), (bb, sb)) in enumerate(zip(ra, rb)):
+            assert ba == bb, f"call {ci} stream {s}: bits differ"
+            assert np.array_equal(sa.view(np.uint32), sb.view(np.uint32)), f"call {ci} stream {s}: symbols"
+
+
 def ring_run(iq2d, calls, sps, span, depth=2, zero_copy=False, **kw):
     """The host-fed ring (qpsk_rx_*): submit every call, collecting only when the
     ring is full, so uploads and computes of consecutive calls overlap."""
