@@ -11,11 +11,6 @@ namespace qpsk {
 constexpr int kModeDemodulate = 0;
 constexpr int kModeConstellation = 1;
 
-// Reversed RRC taps (ComplexFIRFilter._tapsIRev), passed by value -> SGPRs.
-struct TapsRev {
-    float h[kMaxTapsSpecialised];
-};
-
 struct FirArgs {
     const float *x;        // [S][x_stride] float2 input
     int64_t x_stride;      // in float2
@@ -92,7 +87,8 @@ struct IqbArgs {
 };
 
 // Returns true when a specialised tile kernel was used.
-bool launch_fir(const FirArgs &a, const TapsRev &taps, const float *hrev_dev, int T, int W, int S,
+// hrev_dev: the reversed RRC taps (ComplexFIRFilter._tapsIRev) in device memory.
+bool launch_fir(const FirArgs &a, const float *hrev_dev, int T, int W, int S,
                 int64_t n_max, hipStream_t stream);
 void launch_fir_hist(const FirArgs &a, float *hist_new, int H, int S, hipStream_t stream);
 void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant,

@@ -3,7 +3,7 @@
 //
 //   fir_tile_kernel    RRC matched filter (ComplexFIRFilter.Filter, FIRFilter.cs:59-91,
 //                      144-211) for a [stream][time] batch; LDS-staged input tile
-//                      with (T-1)-sample halo, taps in SGPRs, the C# Vector<float>
+//                      with (T-1)-sample halo, taps as uniform scalar loads, the C# Vector<float>
 //                      lane summation order reproduced exactly.
 //   fir_generic_kernel same contract for tap counts / lane widths without a
 //                      specialised instantiation.
@@ -192,7 +192,7 @@ __device__ __forceinline__ void fir_stage(f2 *lds, const f2 *x, const f2 *hist, 
 }
 
 template <int T, int W, int Q, bool VEC, int NT>
-__global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, TapsRev taps, const float *hrev) {
+__global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, const float *hrev) {
     constexpr int TILE = NT * Q;
     constexpr int NIN = TILE + T - 1;
     __shared__ f2 lds[lds_slots(NIN)];
@@ -461,30 +461,30 @@ void launch_append(const AppendArgs &a, hipStream_t stream) {
 // Launchers
 // ---------------------------------------------------------------------------
 template <int T, int NT>
-static void launch_fir_w8_nt(const FirArgs &a, const TapsRev &taps, const float *hrev, int S,
+static void launch_fir_w8_nt(const FirArgs &a, const float *hrev, int S,
                              int64_t n_max, bool vec, hipStream_t stream) {
     constexpr int Q = 8;
     const int64_t tiles = (n_max + NT * Q - 1) / (NT * Q);
     dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(S));
     if (vec)
-        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, true, NT>), grid, dim3(NT), 0, stream, a, taps, hrev);
+        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, true, NT>), grid, dim3(NT), 0, stream, a, hrev);
     else
-        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, false, NT>), grid, dim3(NT), 0, stream, a, taps, hrev);
+        hipLaunchKernelGGL((fir_tile_kernel<T, 8, Q, false, NT>), grid, dim3(NT), 0, stream, a, hrev);
 }
 
 template <int T>
-static bool launch_fir_w8(const FirArgs &a, const TapsRev &taps, const float *hrev, int S,
+static bool launch_fir_w8(const FirArgs &a, const float *hrev, int S,
                           int64_t n_max, bool vec, hipStream_t stream) {
     // 2048-output tiles; 1024- and 512-output tiles (128 / 64 threads, more
     // workgroups beside the loop kernel's) measured the same at C3 and C2
     // (pipelined bench, A/B x2 on one MI355X), and so did a
     // work-sharing tile whose waves take 512-output units from an LDS counter
     // (profiles/r02_fir_share_ab.txt)
-    launch_fir_w8_nt<T, kFirThreads>(a, taps, hrev, S, n_max, vec, stream);
+    launch_fir_w8_nt<T, kFirThreads>(a, hrev, S, n_max, vec, stream);
     return true;
 }
 
-bool launch_fir(const FirArgs &a, const TapsRev &taps, const float *hrev_dev, int T, int W, int S,
+bool launch_fir(const FirArgs &a, const float *hrev_dev, int T, int W, int S,
                 int64_t n_max, hipStream_t stream) {
     if (n_max <= 0 || S <= 0) return true;
     const bool vec = (T % 2 == 1) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) &&
@@ -492,15 +492,15 @@ bool launch_fir(const FirArgs &a, const TapsRev &taps, const float *hrev_dev, in
                      (a.y_stride % 2 == 0) && (a.y_offset % 2 == 0);
     if (W == 8) {
         switch (T) {
-        case 13: return launch_fir_w8<13>(a, taps, hrev_dev, S, n_max, vec, stream);
-        case 17: return launch_fir_w8<17>(a, taps, hrev_dev, S, n_max, vec, stream);
-        case 21: return launch_fir_w8<21>(a, taps, hrev_dev, S, n_max, vec, stream);
-        case 33: return launch_fir_w8<33>(a, taps, hrev_dev, S, n_max, vec, stream);
-        case 41: return launch_fir_w8<41>(a, taps, hrev_dev, S, n_max, vec, stream);
-        case 49: return launch_fir_w8<49>(a, taps, hrev_dev, S, n_max, vec, stream);
-        case 65: return launch_fir_w8<65>(a, taps, hrev_dev, S, n_max, vec, stream);
-        case 97: return launch_fir_w8<97>(a, taps, hrev_dev, S, n_max, vec, stream);
-        case 129: return launch_fir_w8<129>(a, taps, hrev_dev, S, n_max, vec, stream);
+        case 13: return launch_fir_w8<13>(a, hrev_dev, S, n_max, vec, stream);
+        case 17: return launch_fir_w8<17>(a, hrev_dev, S, n_max, vec, stream);
+        case 21: return launch_fir_w8<21>(a, hrev_dev, S, n_max, vec, stream);
+        case 33: return launch_fir_w8<33>(a, hrev_dev, S, n_max, vec, stream);
+        case 41: return launch_fir_w8<41>(a, hrev_dev, S, n_max, vec, stream);
+        case 49: return launch_fir_w8<49>(a, hrev_dev, S, n_max, vec, stream);
+        case 65: return launch_fir_w8<65>(a, hrev_dev, S, n_max, vec, stream);
+        case 97: return launch_fir_w8<97>(a, hrev_dev, S, n_max, vec, stream);
+        case 129: return launch_fir_w8<129>(a, hrev_dev, S, n_max, vec, stream);
         default: break;
         }
     }

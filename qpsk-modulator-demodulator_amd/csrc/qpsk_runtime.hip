@@ -87,7 +87,6 @@ struct qpsk_demod {
     int T = 0;
     int W = 8;
     LoopDesign d;
-    TapsRev taps{};
     LoopParams lp{};
     int loop_variant = 0;
     FllParams fp{};
@@ -287,7 +286,7 @@ int run_fir(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_le
     fa.y = mf; fa.y_stride = h->mf_stride; fa.y_offset = kMfPrefix;
     EV(2, st);
     if (n_call > 0) {
-        launch_fir(fa, h->taps, h->d_hrev, h->T, h->W, h->S, n_call, st);
+        launch_fir(fa, h->d_hrev, h->T, h->W, h->S, n_call, st);
         EV(3, st);
         launch_fir_hist(fa, h->d_hist[h->hist_cur ^ 1], h->T - 1, h->S, st);
         h->hist_cur ^= 1;
@@ -476,7 +475,6 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
         return fail(rc, err);
     }
     h->T = static_cast<int>(h->d.rrc_f32.size());
-    for (int k = 0; k < h->T && k < kMaxTapsSpecialised; ++k) h->taps.h[k] = h->d.rrc_f32[h->T - 1 - k];
     h->lp.sps = h->d.mm_sps;
     h->lp.kp = h->d.kp;
     h->lp.ki = h->d.ki;

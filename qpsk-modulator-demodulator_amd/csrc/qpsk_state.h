@@ -18,7 +18,6 @@ namespace qpsk {
 constexpr int kCarryMax = 64;      // retained M&M samples between calls (normally 3)
 constexpr int kMfPrefix = 64;      // MF buffer prefix that receives the carry
 constexpr int kFllTaps = 40;       // QPSKDeModulator.cs:35
-constexpr int kMaxTapsSpecialised = 260;
 
 struct alignas(16) StreamState {
     double mu;          // MuellerMuller.mu
