@@ -91,8 +91,9 @@ struct IqbArgs {
 bool launch_fir(const FirArgs &a, const float *hrev_dev, int T, int W, int S,
                 int64_t n_max, hipStream_t stream);
 void launch_fir_hist(const FirArgs &a, float *hist_new, int H, int S, hipStream_t stream);
+// after_carry (optional): recorded between the carry kernel and the loop kernel
 void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant,
-                 hipStream_t stream);
+                 hipStream_t stream, hipEvent_t after_carry = nullptr);
 void launch_append(const AppendArgs &a, hipStream_t stream);
 void launch_iq_balance(const IqbArgs &a, hipStream_t stream);
 void launch_fll(const FllArgs &a, const FllParams &P, hipStream_t stream);

@@ -844,8 +844,9 @@ static void launch_loop_spw(const LoopArgs &a, const LoopParams &P, int mode, hi
 }
 
 void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant,
-                 hipStream_t stream) {
+                 hipStream_t stream, hipEvent_t after_carry) {
     hipLaunchKernelGGL(carry_prefix_kernel, dim3(a.S), dim3(64), 0, stream, a);
+    if (after_carry) (void)hipEventRecord(after_carry, stream);
     // The loop is latency-bound per stream; a wave's lanes are free, so the
     // default (sps >= 2) is 32 streams x 64-sample rounds.  Measured at C2
     // (profiles/r01_loop_probe.txt): 16 x 64 and 16 x 128 (half the barriers)

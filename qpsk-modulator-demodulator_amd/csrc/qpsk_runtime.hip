@@ -138,6 +138,11 @@ struct qpsk_demod {
     hipEvent_t e_in = nullptr;
     hipEvent_t e_front[2] = {nullptr, nullptr}, e_back[2] = {nullptr, nullptr};
     bool front_rec[2] = {false, false}, back_rec[2] = {false, false};
+    // FLL off: recorded on the back stream between the carry kernel and the
+    // loop kernel; the next call's FIR waits for it, so the loop kernel is
+    // dispatched first (see process_async_one)
+    hipEvent_t e_carry[2] = {nullptr, nullptr};
+    bool carry_rec[2] = {false, false};
     int last_back = -1;              // boundary buffer of the newest back stage, -1 = none
     int64_t *h_len[2] = {nullptr, nullptr};   // pinned staging of per-call lengths
 };
@@ -298,7 +303,7 @@ int run_fir(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_le
 
 // symbol sync + Costas + decode (QPSKDeModulator.cs:364-408) and the output copies
 int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipStream_t st,
-             hipEvent_t *ev) {
+             hipEvent_t *ev, hipEvent_t after_carry = nullptr) {
     const int S = h->S;
     EV(4, st);
     LoopArgs la{};
@@ -317,7 +322,7 @@ int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipS
     la.S = S;
     la.flags = h->d_flags + (c.mem == QPSK_MEM_HOST && !c.append ? 1 : 0);
     la.chunked = c.append ? 1 : 0;
-    launch_loop(la, h->lp, c.mode, h->loop_variant, st);
+    launch_loop(la, h->lp, c.mode, h->loop_variant, st, after_carry);
     HIP_TRY(hipGetLastError());
     EV(5, st);
     if (c.append) {
@@ -384,6 +389,7 @@ int pipe_setup(qpsk_demod *h) {
     for (int b = 0; b < 2; ++b) {
         HIP_TRY(hipEventCreateWithFlags(&h->e_front[b], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&h->e_back[b], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&h->e_carry[b], hipEventDisableTiming));
         HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h->h_len[b]), h->S * sizeof(int64_t)));
     }
     int rc;
@@ -585,6 +591,7 @@ int qpsk_demod_destroy(qpsk_demod *h) {
         if (h->h_len[b]) hipHostFree(h->h_len[b]);
         if (h->e_front[b]) hipEventDestroy(h->e_front[b]);
         if (h->e_back[b]) hipEventDestroy(h->e_back[b]);
+        if (h->e_carry[b]) hipEventDestroy(h->e_carry[b]);
     }
     hipFree(h->d_carry);
     hipFree(h->d_iqb);
@@ -753,7 +760,17 @@ int process_async_one(qpsk_demod *h, const Call &c) {
                           n_call, mf, B, ev)))
             return rc;
     } else {
-        // front = FIR into MF rows b; back = loop
+        // front = FIR into MF rows b; back = loop.  FIR(k+1) and loop(k) both
+        // become ready when a stage of call k-1 or k ends, and whichever is
+        // dispatched first takes the CUs: a loop kernel dispatched after the
+        // FIR finds no CU with room for its 125 KB workgroups and runs after
+        // it (measured on MI355X at C3: FIR 42 + loop 80 ms a call, against
+        // FIR 52 || loop 43 the other way round, profiles/r02_c3_dispatch_race.txt),
+        // and either order then repeats itself call after call.  So FIR(k+1)
+        // also waits for the carry kernel that precedes loop(k) on the back
+        // stream: the loop kernel is dispatched as that event signals.
+        if (h->last_back >= 0 && h->carry_rec[h->last_back])
+            HIP_TRY(hipStreamWaitEvent(F, h->e_carry[h->last_back], 0));
         EV(1, F);
         mf = h->d_mf[b];
         if ((rc = run_fir(h, x, x_stride, d_len, n_call, mf, F, ev))) return rc;
@@ -761,7 +778,8 @@ int process_async_one(qpsk_demod *h, const Call &c) {
         HIP_TRY(hipStreamWaitEvent(B, h->e_front[b], 0));
     }
     h->front_rec[b] = true;
-    if ((rc = run_loop(h, c, d_len, mf, B, ev))) return rc;
+    if ((rc = run_loop(h, c, d_len, mf, B, ev, h->p.enable_fll ? nullptr : h->e_carry[b]))) return rc;
+    h->carry_rec[b] = !h->p.enable_fll;
     HIP_TRY(hipEventRecord(h->e_back[b], B));
     h->back_rec[b] = true;
     h->last_back = b;
