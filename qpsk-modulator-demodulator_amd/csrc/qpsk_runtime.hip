@@ -764,9 +764,10 @@ int process_async_one(qpsk_demod *h, const Call &c) {
         // become ready when a stage of call k-1 or k ends, and whichever is
         // dispatched first takes the CUs: a loop kernel dispatched after the
         // FIR finds no CU with room for its 125 KB workgroups and runs after
-        // it (measured on MI355X at C3: FIR 42 + loop 80 ms a call, against
-        // FIR 52 || loop 43 the other way round, profiles/r02_c3_dispatch_race.txt),
-        // and either order then repeats itself call after call.  So FIR(k+1)
+        // it (measured on MI355X at C3 under rocprofv3: FIR 42 + loop 80 ms a
+        // call, against FIR 52 || loop 43 the other way round,
+        // profiles/r02_c3_dispatch_race.txt), and either order then repeats
+        // itself call after call.  So FIR(k+1)
         // also waits for the carry kernel that precedes loop(k) on the back
         // stream: the loop kernel is dispatched as that event signals.
         if (h->last_back >= 0 && h->carry_rec[h->last_back])
