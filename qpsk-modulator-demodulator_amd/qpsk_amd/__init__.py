@@ -40,6 +40,10 @@ MEM_HOST = 0
 MEM_DEVICE = 1
 MODE_DEMODULATE = 0
 MODE_CONSTELLATION = 1
+# the Costas loop's double sin/cos (CostasLoopQpsk.cs:69-70) on the GPU is
+# glibc's own sin/cos (bit-identical symbols vs the libm oracle) when True,
+# the portable table sincos (within 1 ulp of glibc) when False
+COSTAS_TRIG_EXACT = False
 
 _i64p = C.POINTER(C.c_int64)
 _u8p = C.POINTER(C.c_uint8)

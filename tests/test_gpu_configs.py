@@ -1,0 +1,127 @@
+"""GPU parity at the BASELINE.json workloads, at full size.
+
+C3 (4096 x 2^20, sps 4, 129 taps), the C4 shard (4096 x 2^20, sps 8, 65 taps)
+and C5 (8192 x 2^20, +-5 kHz CFO + multipath + AWGN, FLL on) run on the HIP
+path exactly as bench.py synthesises them (same generator, seeds and LO
+pair), through QPSKDeModulator.DeModulate semantics (QPSKDeModulator.cs:345-425):
+seven consecutive calls on the same buffer, as the bench's timed region
+feeds it.  Each call's bit rows of the first 8 and the last 8 streams (row
+offsets 32-64 GiB into the buffers), plus the 4 streams whose Costas phase
+grew the most (QPSK false lock: |freq| near a multiple of pi/2, theta growing
+every symbol past the single +-2pi wrap of CostasLoopQpsk.cs:90-91, so the
+large-|theta| reduction paths run), are compared with the CPU oracle calling
+the real glibc trig (what .NET's Math.Sin/Cos and MathF.Sin/Cos reach on
+Linux), one oracle demodulator per stream fed the same seven calls.
+
+Bar: bits identical on every call; rotated symbols of the first (fresh
+state) and the seventh (steady state) call identical, or within SYM_TOL where
+the GPU's Costas sincos is not glibc's (qpsk_amd.COSTAS_TRIG_EXACT).
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import common as K
+import oracle as O
+import qpsk_amd as Q
+from test_gpu_parity import SYM_TOL
+
+pytestmark = pytest.mark.gpu
+
+N = 1 << 20
+CALLS = 7
+SEED = 0x5159534B            # bench.py synth_kw
+STATE_REC = 112              # sizeof(StreamState), csrc/qpsk_state.h
+THETA_IDX = 2                # StreamState.theta as the 3rd double of a record
+
+CASES = {
+    # key: streams, sps, rrc span, impaired channel + FLL, pipelined calls
+    "c3": dict(S=4096, sps=4, span=32, impaired=False, pipelined=True),
+    "c4_shard": dict(S=4096, sps=8, span=8, impaired=False, pipelined=False),
+    "c5": dict(S=8192, sps=8, span=8, impaired=True, pipelined=False),
+}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need an MI355X")
+    yield
+    torch.cuda.empty_cache()
+
+
+def _rows(t, idx):
+    return np.concatenate([t[i: i + 1].cpu().numpy() for i in idx])
+
+
+def _oracle_stream(row, sps, span, fll):
+    """CALLS DeModulate calls of one oracle instance on the same row."""
+    d = K.oracle_for(sps, span, trig=O.TRIG_LIBM, enable_fll=fll)
+    return [d.demodulate_ex(row) for _ in range(CALLS)]
+
+
+@pytest.mark.parametrize("key", list(CASES))
+def test_baseline_workload_seven_calls_vs_libm_oracle(key):
+    import torch
+    c = CASES[key]
+    S, sps, span, imp = c["S"], c["sps"], c["span"], c["impaired"]
+    dev = torch.device("cuda", 0)
+    iq, _tx = Q.synth_generate(S, N, K.FS, K.FS // sps, rrc_alpha=K.ALPHA, rrc_span=span, seed=SEED,
+                               lo_ppm=1.0, cfo_hz=5000.0 if imp else 0.0, multipath=imp,
+                               esn0_db=20.0 if imp else None)
+    del _tx
+    assert iq.stride(0) * 4 * (S - 1) > (16 << 30)   # last rows 32-64 GiB in
+    b = Q.BatchDemodulator(S, Q.params(K.FS, K.FS // sps, K.ALPHA, span, enable_fll=imp,
+                                       max_samples_per_call=N))
+    ms = b.max_symbols(N)
+    stream = torch.cuda.Stream(dev)
+    b.set_stream(stream.cuda_stream)
+    outs = []
+    for k in range(CALLS):
+        bits = torch.zeros((S, (2 * ms + 7) // 8 + 8), dtype=torch.uint8, device=dev)
+        nb = torch.zeros(S, dtype=torch.int64, device=dev)
+        sy = ns = None
+        if k in (0, CALLS - 1):
+            sy = torch.zeros((S, 2 * ms), dtype=torch.float32, device=dev)
+            ns = torch.zeros(S, dtype=torch.int64, device=dev)
+        outs.append((bits, nb, sy, ns))
+    torch.cuda.synchronize(dev)
+    with torch.cuda.stream(stream):
+        for bits, nb, sy, ns in outs:
+            if c["pipelined"]:
+                b.process_device_async(iq, N, bits, nb, syms_dev=sy, n_syms_dev=ns)
+            else:
+                b.process_device(iq, N, bits, nb, syms_dev=sy, n_syms_dev=ns)
+        if c["pipelined"]:
+            b.pipeline_wait()
+    stream.synchronize()
+    assert b.status() == 0
+    theta = np.frombuffer(b.get_state()[: S * STATE_REC], dtype=np.float64).reshape(S, -1)[:, THETA_IDX]
+    idx = list(range(8)) + list(range(S - 8, S))
+    idx += [int(i) for i in np.argsort(-np.abs(theta)) if int(i) not in idx][:4]
+    host = _rows(iq, idx)
+    got = []
+    for bits, nb, sy, ns in outs:
+        got.append((_rows(bits, idx), _rows(nb, idx), None if sy is None else _rows(sy, idx),
+                    None if ns is None else _rows(ns, idx)))
+    b.close()
+    del outs, iq
+    torch.cuda.empty_cache()
+
+    with ThreadPoolExecutor(max_workers=len(idx)) as ex:
+        ref = list(ex.map(lambda r: _oracle_stream(r, sps, span, imp), list(host)))
+    exact = Q.COSTAS_TRIG_EXACT
+    for j, s in enumerate(idx):
+        for k in range(CALLS):
+            gb, gnb, gsy, gns = (x[j] if x is not None else None for x in got[k])
+            rb, rsy, _ = ref[j][k]
+            assert Q.unpack_bits(gb, int(gnb)) == rb, f"{key} stream {s} (|theta| {abs(theta[s]):.3g}) call {k}: bits"
+            if gsy is not None:
+                g = gsy[: 2 * int(gns)]
+                assert g.shape == rsy.shape, f"{key} stream {s} call {k}: symbol count"
+                if exact:
+                    assert np.array_equal(g, rsy), f"{key} stream {s} call {k}: symbols"
+                else:
+                    assert np.max(np.abs(g - rsy), initial=0) <= SYM_TOL, f"{key} stream {s} call {k}"
