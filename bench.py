@@ -180,10 +180,13 @@ def pick_streams(S, n_cover, tail=64):
     return list(range(head)) + list(range(S - tail, S))
 
 
-def cpu_leg(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, n, budget_s, threads, single_streams=8):
+def cpu_leg(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, n, budget_s, threads, single_streams=8,
+            n_cover=None):
     """CPU baseline + parity at scale: the oracle (glibc trig) on the host
     cores over a time-bounded subset of the timed batch, timed, and its bit
-    rows / symbols compared with the GPU's rows of the same streams."""
+    rows / symbols compared with the GPU's rows of the same streams.
+    n_cover: a fixed stream count instead of the time budget (N > 1: every
+    rank checks the first 8 and the last 64 streams of its shard)."""
     import numpy as np
     import torch
     import oracle as O
@@ -198,7 +201,8 @@ def cpu_leg(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, n, budget_s, thre
     dt1 = time.perf_counter() - t0
     per_stream = dt1 / ns1
     eff = min(threads, cpu_quota() or threads)
-    n_cover = max(min(S, 64 + 8), int(budget_s * eff / per_stream))
+    if n_cover is None:
+        n_cover = max(min(S, 64 + 8), int(budget_s * eff / per_stream))
     idx = pick_streams(S, n_cover)
     host = rows_to_host(iq, idx)
     want_syms = syms_dev is not None
@@ -443,11 +447,34 @@ def framer_pass(bits, nbits, S, stream, reps=5):
             "bits_GBps": round(row_bytes / (t_push / reps * 1e-3) / 1e9, 1) if t_push > 0 else None}
 
 
-def rooflines(st, S, n, cfg):
-    """Per-kernel rooflines from the stage events of the timed region
-    (algorithmic bytes / flops per unit)."""
+TIMING_SOURCE = ("in-kernel launch timestamps over the timed region: each launch's first workgroup "
+                 "start to last workgroup end on the device's 100 MHz wall clock (s_memrealtime), "
+                 "the span a kernel trace reports, on whichever stream the kernel ran")
+
+
+def launch_stats(col):
+    """Per-kernel launch statistics of one column of launch_times() (ms);
+    slow_launches = launches longer than 1.3x the median (a lost dispatch
+    race, a co-scheduling swing)."""
+    import numpy as np
+    v = np.asarray(col, dtype=np.float64)
+    v = v[v > 0]
+    if not v.size:
+        return None
+    med = float(np.median(v))
+    return {"launches": int(v.size), "ms_mean": round(float(v.mean()), 4), "ms_median": round(med, 4),
+            "ms_min": round(float(v.min()), 4), "ms_max": round(float(v.max()), 4),
+            "ms_std": round(float(v.std()), 4), "slow_launches": int((v > 1.3 * med).sum())}
+
+
+def rooflines(st, S, n, cfg, lt=None):
+    """Per-kernel rooflines of the timed region (algorithmic
+    bytes / flops per unit ÷ the kernel's mean launch time from the in-kernel
+    timestamps).  lt: launch_times() rows of the timed calls."""
     sps, T = cfg["sps"], cfg["span"] * cfg["sps"] + 1
     out = {}
+    col = {"fll": 0, "fir": 1, "loop": 2}
+    stats = {k: (launch_stats(lt[:, i]) if lt is not None and len(lt) else None) for k, i in col.items()}
     if st["fir"] > 0:
         fir_s = st["fir"] / 1e3
         gbs = 16.0 * S * n / fir_s / 1e9             # 8 B in + 8 B out per complex sample
@@ -459,7 +486,8 @@ def rooflines(st, S, n, cfg):
                       "valu_frac": round(tfl / FP32_PEAK_TFLOPS, 4),
                       "valu_peak_unfused_tflops": FP32_PEAK_UNFUSED_TFLOPS,
                       "valu_frac_unfused": round(tfl / FP32_PEAK_UNFUSED_TFLOPS, 4),
-                      "per_unit": f"16 B and {4 * T} flop per complex sample, {S * n} samples per launch"}
+                      "per_unit": f"16 B and {4 * T} flop per complex sample, {S * n} samples per launch",
+                      "launch_stats": stats["fir"]}
     if st["loop"] > 0:
         loop_s = st["loop"] / 1e3
         b = (8.0 + 0.25 / sps) * S * n               # MF samples in + packed bits out
@@ -470,8 +498,9 @@ def rooflines(st, S, n, cfg):
                        "frac": round(b / loop_s / 1e9 / HBM_PEAK_GBS, 4),
                        "ns_per_symbol_per_stream": round(loop_s / (n / sps) * 1e9, 2),
                        "per_unit": f"{8 + 0.25 / sps:.4f} B per complex sample, {S * n} samples, "
-                                   f"{int(syms)} symbols per launch"}
-    if st["fll"] > 0.01:
+                                   f"{int(syms)} symbols per launch",
+                       "launch_stats": stats["loop"]}
+    if cfg["fll"] and st["fll"] > 0:
         fll_s = st["fll"] / 1e3
         tfl = 640.0 * S * n / fll_s / 1e12
         out["fll"] = {"kernel": "fll_sys_kernel (Band-Edge FLL)", "ms": round(st["fll"], 4),
@@ -479,7 +508,10 @@ def rooflines(st, S, n, cfg):
                       "achieved": round(16.0 * S * n / fll_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                       "unit": "GB/s", "frac": round(16.0 * S * n / fll_s / 1e9 / HBM_PEAK_GBS, 4),
                       "valu_tflops": round(tfl, 2), "valu_frac": round(tfl / FP32_PEAK_TFLOPS, 4),
-                      "per_unit": "16 B and 640 flop (+ one sincos) per complex sample"}
+                      "per_unit": "16 B and 640 flop (+ one sincos) per complex sample",
+                      "launch_stats": stats["fll"]}
+    for v in out.values():
+        v["source"] = TIMING_SOURCE
     return out
 
 
@@ -549,11 +581,13 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     st = demod.stage_times()
+    lt = demod.launch_times()
     demod.enable_timing(False)
 
     rec = {}
     errs = total_bits = lost = slips = 0
     bad_bits = bad_syms = n_port = 0
+    libm_bad = libm_streams = 0
     if not args.timed_only:
         # untimed: one call from the initial state on every stream of the timed
         # handle (stream starts at t=0); its rows feed parity and BER
@@ -572,17 +606,31 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
             idx = [0, 1, S - 2, S - 1] if S >= 4 else list(range(S))
             bad_bits, bad_syms = portable_check(iq, bits, nbits, syms, nsyms, cfg, idx)
             n_port = len(idx)
-            if rank == 0 and world == 1 and not args.no_cpu_baseline:
-                threads = args.cpu_threads or (os.cpu_count() or 1)
-                rec["cpu_baseline"], rec["parity_vs_libm_oracle"] = cpu_leg(
-                    iq, bits, nbits, syms, nsyms, cfg, n, args.cpu_seconds, threads)
+            if not args.no_cpu_baseline:
+                # every rank: the libm oracle on its own shard (N = 1: as many
+                # streams as the CPU budget allows; N > 1: the first 8 and last
+                # 64 of the shard, on this rank's share of the host threads)
+                threads = args.cpu_threads or max(1, (os.cpu_count() or 1) // world)
+                cpu, par = cpu_leg(iq, bits, nbits, syms, nsyms, cfg, n, args.cpu_seconds, threads,
+                                   n_cover=None if world == 1 else min(S, 72))
+                libm_bad, libm_streams = par["mismatching_streams"], par["streams"]
+                if rank == 0:
+                    rec["cpu_baseline"], rec["parity_vs_libm_oracle"] = cpu, par
         del syms, nsyms
-    t_max, (errs, total_bits, lost, slips, bad_bits, bad_syms, n_port) = reduce_stats(
-        elapsed, [errs, total_bits, lost, slips, bad_bits, bad_syms, n_port],
+    t_max, (errs, total_bits, lost, slips, bad_bits, bad_syms, n_port, libm_bad, libm_streams) = reduce_stats(
+        elapsed, [errs, total_bits, lost, slips, bad_bits, bad_syms, n_port, libm_bad, libm_streams],
         device=dev if nccl else None)
+    if world > 1 and "parity_vs_libm_oracle" in rec:
+        par = rec["parity_vs_libm_oracle"]
+        par["rank0"] = {k: par.pop(k) for k in ("first_stream", "last_stream", "mismatch_examples",
+                                                  "max_row_offset_GiB") if k in par}
+        par["streams"] = libm_streams
+        par["mismatching_streams"] = libm_bad
+        par["scope"] = (f"every rank: the first 8 and the last 64 streams of its {S}-stream shard, "
+                        f"summed over {world} ranks")
 
     value = world * S * n * steps / t_max / 1e6
-    rl = rooflines(st, S, n, cfg)
+    rl = rooflines(st, S, n, cfg, lt)
     dom = max(rl, key=lambda k: rl[k]["ms"]) if rl else None
     roof = None
     if dom:
@@ -694,8 +742,9 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
                     help="headline workload (default C3, the largest single-GPU config)")
     ap.add_argument("--sub-configs", default="auto",
-                    help="comma list run after the headline as sub_records; 'auto' = c2,c5 at N=1, "
-                         "c4 at N>1; 'none' = headline only")
+                    help="comma list run after the headline as sub_records; 'auto' = c2,c4,c5 at N=1 "
+                         "(c4: the per-GPU shard of BASELINE's 8-GPU config, the N = 1 point of its "
+                         "curve), c4 at N>1; 'none' = headline only")
     ap.add_argument("--sub-steps", type=int, default=5)
     ap.add_argument("--samples", type=int, default=1 << 20)
     ap.add_argument("--loop-variant", type=int, default=0,
@@ -756,7 +805,7 @@ def main():
     out = run_config(args.config, args, rank, world, dev, args.steps, args.warmup, headline=True)
     subs = args.sub_configs
     if subs == "auto":
-        subs = "c2,c5" if world == 1 else "c4"
+        subs = "c2,c4,c5" if world == 1 else "c4"
     sub = {}
     for key in [k for k in subs.split(",") if k and k != "none" and k != args.config]:
         r = run_config(key, args, rank, world, dev, args.sub_steps, 1, headline=False)

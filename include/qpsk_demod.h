@@ -174,12 +174,20 @@ int64_t qpsk_demod_max_symbols(const qpsk_demod *h, int64_t n_samples);
  * Returns the bit index just past the TSC, or -1. */
 int64_t qpsk_tsc_find(const uint8_t *bits, int64_t n_bits, const char *tsc);
 
-/* Per-stage device times (ms) of the last process() call, measured with HIP
- * events on the handle's stream when timing is enabled.
- * ms[0] = FLL, ms[1] = matched-filter FIR, ms[2] = symbol-sync + Costas + decode,
- * ms[3] = whole call.  Returns the number of entries written. */
+/* Kernel launch times of the calls issued since timing was enabled (the first
+ * 4096 of them), recorded by the kernels themselves: first workgroup start to
+ * last workgroup end on the device's 100 MHz wall clock, so a launch's time is
+ * its own span whichever stream or neighbour it ran beside (pipelined calls
+ * included).  enable_timing(on) restarts the record.
+ * stage_times: averages over the recorded calls of ms[0] = FLL, ms[1] =
+ * matched-filter FIR, ms[2] = symbol-sync + Costas + decode kernel, ms[3] =
+ * the call's kernel span (earliest start to latest end); a kernel that did not
+ * run counts as absent.  Returns the number of entries written (<= 4).
+ * launch_times: the same four values per call, ms[4*k .. 4*k+3] for call k
+ * (0 = did not run); returns the number of calls written (<= max_calls). */
 int qpsk_demod_enable_timing(qpsk_demod *h, int32_t on);
-int qpsk_demod_stage_times(const qpsk_demod *h, float *ms, int32_t n);
+int qpsk_demod_stage_times(qpsk_demod *h, float *ms, int32_t n);
+int qpsk_demod_launch_times(qpsk_demod *h, float *ms, int32_t max_calls);
 
 /* Design products, for parity checks against the reference constructor. */
 int qpsk_demod_rrc_taps(const qpsk_demod *h, float *taps, int32_t cap);

@@ -112,6 +112,7 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
     constexpr int N = kFllTaps;
     static_assert(N == 40, "systolic FLL assumes 5 blocks of 8 taps");
     __shared__ FllSysLds L;
+    if (a.kt && threadIdx.x == 0) kt_start(a.kt);
     if (threadIdx.x < 2 * N) L.taps[threadIdx.x] = P.lower_rev[threadIdx.x];
 
     const int lane = threadIdx.x & 63;
@@ -408,6 +409,7 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
             stp->fll_pos = pos_end;
         }
     }
+    if (a.kt && lane == 0) kt_end(a.kt);
 }
 
 void launch_fll_sys(const FllArgs &a, const FllParams &P, hipStream_t stream) {

@@ -11,6 +11,21 @@ namespace qpsk {
 constexpr int kModeDemodulate = 0;
 constexpr int kModeConstellation = 1;
 
+// Launch timestamps (qpsk_demod_enable_timing): kt[0] = the earliest
+// workgroup start, kt[1] = the latest workgroup end of one kernel launch, in
+// ticks of the 100 MHz wall clock (s_memrealtime; hipDeviceAttributeWallClockRate).
+// The kernel's own span, as a kernel trace reports it, whichever streams its
+// neighbours run on; recorded with vector atomics by a few lanes per launch.
+__device__ __forceinline__ void kt_start(unsigned long long *kt) { atomicMin(kt, wall_clock64()); }
+__device__ __forceinline__ void kt_end(unsigned long long *kt) { atomicMax(kt + 1, wall_clock64()); }
+// records kt_end when it goes out of scope (every return path), lane 0 of each wave
+struct KtEnd {
+    unsigned long long *kt;
+    __device__ ~KtEnd() {
+        if (kt && (threadIdx.x & 63) == 0) kt_end(kt);
+    }
+};
+
 struct FirArgs {
     const float *x;        // [S][x_stride] float2 input
     int64_t x_stride;      // in float2
@@ -20,6 +35,7 @@ struct FirArgs {
     float *y;              // [S][y_stride] float2 output at y_offset
     int64_t y_stride;
     int64_t y_offset;
+    unsigned long long *kt;   // launch timestamps or nullptr
 };
 
 struct LoopArgs {
@@ -41,6 +57,11 @@ struct LoopArgs {
     unsigned long long *probe;   // diagnostic cycle stamps (QPSK_LOOP_STAMPS builds only)
     uint32_t *flags;       // per-handle OR of QPSK_STATUS_* raised by this call (or nullptr)
     int chunked;           // 1: an internal chunk of a longer call (StreamState.tofs runs on)
+    unsigned long long *kt;   // launch timestamps or nullptr
+    // residency counter (signal memory) or nullptr: every workgroup adds 1 as it
+    // starts, so the next pipelined call's FIR can wait until the loop kernel
+    // holds its CUs (qpsk_runtime.hip, process_async_one)
+    unsigned long long *resident;
 };
 
 // One internal chunk's rows appended behind what earlier chunks of the same
@@ -73,6 +94,7 @@ struct FllArgs {
     int64_t n;
     StreamState *state;
     int S;
+    unsigned long long *kt;   // launch timestamps or nullptr
 };
 
 struct IqbArgs {
@@ -91,9 +113,8 @@ struct IqbArgs {
 bool launch_fir(const FirArgs &a, const float *hrev_dev, int T, int W, int S,
                 int64_t n_max, hipStream_t stream);
 void launch_fir_hist(const FirArgs &a, float *hist_new, int H, int S, hipStream_t stream);
-// after_carry (optional): recorded between the carry kernel and the loop kernel
-void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant,
-                 hipStream_t stream, hipEvent_t after_carry = nullptr);
+// carry kernel + loop kernel; returns the loop kernel's workgroup count
+int launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant, hipStream_t stream);
 void launch_append(const AppendArgs &a, hipStream_t stream);
 void launch_iq_balance(const IqbArgs &a, hipStream_t stream);
 void launch_fll(const FllArgs &a, const FllParams &P, hipStream_t stream);

@@ -40,6 +40,7 @@ __device__ __forceinline__ int lds_slot(int i) { return i + ((i >> 6) << 3); }
 constexpr int lds_slots(int n) { return n + ((n >> 6) << 3) + 8; }
 
 constexpr int kFirThreads = 256;
+constexpr unsigned kKtLastWgs = 8192;
 
 // One output of the tile with the reference's full complex products
 // (FIRFilter.cs:165-192): lane accumulators from +0, (hI*xI) - (hQ*xQ) and
@@ -200,10 +201,19 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, const float *hr
     const int s = blockIdx.y;
     const int64_t tile0 = static_cast<int64_t>(blockIdx.x) * TILE;
     const int64_t n = a.lengths ? a.lengths[s] : a.n;
-    if (tile0 >= n) return;
+    const int tid = threadIdx.x;
+    // launch timestamps: workgroups are dispatched in linear order, so the
+    // launch starts with the first ones and ends with one of the last
+    // kKtLastWgs (a few workgroup lifetimes of the whole chip)
+    const unsigned lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const bool kt_last = a.kt && tid == 0 && lin + kKtLastWgs >= gridDim.x * gridDim.y;
+    if (a.kt && tid == 0 && lin < 64) kt_start(a.kt);
+    if (tile0 >= n) {
+        if (kt_last) kt_end(a.kt);
+        return;
+    }
     const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
     const f2 *hist = reinterpret_cast<const f2 *>(a.hist) + static_cast<int64_t>(s) * (T - 1);
-    const int tid = threadIdx.x;
 
     fir_stage<T, NIN, VEC, NT>(lds, x, hist, tile0, n);
     __syncthreads();
@@ -254,6 +264,7 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, const float *hr
             y[go] = fir_exact_one(xs, hrev, T, W);
         }
     }
+    if (kt_last) kt_end(a.kt);
 }
 
 // Any (T, W) without a specialised tile kernel: the reference's formula
@@ -263,6 +274,9 @@ __global__ __launch_bounds__(256) void fir_generic_kernel(FirArgs a, const float
     const int s = blockIdx.y;
     const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const int64_t n = a.lengths ? a.lengths[s] : a.n;
+    const unsigned lin = blockIdx.y * gridDim.x + blockIdx.x;
+    if (a.kt && threadIdx.x == 0 && lin < 64) kt_start(a.kt);
+    KtEnd kte{lin + kKtLastWgs >= gridDim.x * gridDim.y ? a.kt : nullptr};
     if (t >= n) return;
     const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
     const f2 *hist = reinterpret_cast<const f2 *>(a.hist) + static_cast<int64_t>(s) * (T - 1);
@@ -328,6 +342,8 @@ __device__ __forceinline__ void fll_dot(const float *taps_rev, const f2 *win, in
 }
 
 __global__ __launch_bounds__(64) void fll_kernel(FllArgs a, FllParams P) {
+    if (a.kt && threadIdx.x == 0) kt_start(a.kt);
+    KtEnd kte{a.kt};
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= a.S) return;
     const int64_t n = a.lengths ? a.lengths[s] : a.n;

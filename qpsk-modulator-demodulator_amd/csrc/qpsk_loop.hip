@@ -160,6 +160,15 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
+    if (wave == 1 && lane == 0) {
+        if (a.kt) kt_start(a.kt);
+        // this workgroup holds its CU now: the next pipelined call's FIR waits
+        // for min(grid, CUs) of these (qpsk_runtime.hip, process_async_one)
+        if (a.resident) __hip_atomic_fetch_add(a.resident, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // the stage waves record the launch end as they leave (not the loader, whose
+    // vmcnt waits count its own outstanding memory operations)
+    KtEnd kte{wave != 0 ? a.kt : nullptr};
     // the batch spread evenly over the grid: workgroup b owns streams
     // [b S / G, (b + 1) S / G), at most SPW.  A workgroup left with few
     // streams (e.g. 16 of 24 at S = 256) runs its uniform loops ~10-25 %
@@ -827,7 +836,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
 }
 
 template <int SPW, int CAP, int KB>
-static void launch_loop_spw(const LoopArgs &a, const LoopParams &P, int mode, hipStream_t stream) {
+static int launch_loop_spw(const LoopArgs &a, const LoopParams &P, int mode, hipStream_t stream) {
     dim3 grid((a.S + SPW - 1) / SPW), block(256);
     const bool syms = a.syms != nullptr;
     const bool diff = P.differential != 0;
@@ -841,12 +850,11 @@ static void launch_loop_spw(const LoopArgs &a, const LoopParams &P, int mode, hi
         hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, true, SPW, CAP, KB>), grid, block, 0, stream, a, P);
     else
         hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, false, SPW, CAP, KB>), grid, block, 0, stream, a, P);
+    return static_cast<int>(grid.x);
 }
 
-void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant,
-                 hipStream_t stream, hipEvent_t after_carry) {
+int launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant, hipStream_t stream) {
     hipLaunchKernelGGL(carry_prefix_kernel, dim3(a.S), dim3(64), 0, stream, a);
-    if (after_carry) (void)hipEventRecord(after_carry, stream);
     // The loop is latency-bound per stream; a wave's lanes are free, so the
     // default (sps >= 2) is 32 streams x 64-sample rounds.  Measured at C2
     // (profiles/r01_loop_probe.txt): 16 x 64 and 16 x 128 (half the barriers)
@@ -854,19 +862,19 @@ void launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant,
     // which fits LDS at 16 streams x 64.  variant (qpsk_demod_params.loop_variant)
     // forces 1 = 16 x 64, 2 = 32 x 64, 3 = 16 x 128; all compute identical results.
     if (P.sps < 2.0)
-        launch_loop_spw<16, kCapAny, 64>(a, P, mode, stream);
+        return launch_loop_spw<16, kCapAny, 64>(a, P, mode, stream);
     else if (variant == 1)
-        launch_loop_spw<16, kCapSps2, 64>(a, P, mode, stream);
+        return launch_loop_spw<16, kCapSps2, 64>(a, P, mode, stream);
     else if (variant == 3)
-        launch_loop_spw<16, kCap128Sps2, 128>(a, P, mode, stream);
+        return launch_loop_spw<16, kCap128Sps2, 128>(a, P, mode, stream);
     else if (variant == 4 && P.sps >= 8.0)
-        launch_loop_spw<24, kCap128Sps8, 128>(a, P, mode, stream);
+        return launch_loop_spw<24, kCap128Sps8, 128>(a, P, mode, stream);
     else if (P.sps >= 8.0)
-        launch_loop_spw<32, kCapSps8, 64>(a, P, mode, stream);
+        return launch_loop_spw<32, kCapSps8, 64>(a, P, mode, stream);
     else if (P.sps >= 4.0)
-        launch_loop_spw<32, kCapSps4, 64>(a, P, mode, stream);
+        return launch_loop_spw<32, kCapSps4, 64>(a, P, mode, stream);
     else
-        launch_loop_spw<32, kCapSps2, 64>(a, P, mode, stream);
+        return launch_loop_spw<32, kCapSps2, 64>(a, P, mode, stream);
 }
 
 }  // namespace qpsk

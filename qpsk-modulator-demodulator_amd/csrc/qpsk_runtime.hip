@@ -29,11 +29,13 @@
 //   state   [S]                     StreamState
 //   bits    [S][words]              uint32  MSB-first packed bits
 //   syms    [S][syms_cap]           float2  rotated symbols (on request)
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -70,7 +72,10 @@ int dev_alloc(T **p, size_t count) {
     return QPSK_OK;
 }
 
-constexpr int kEv = 6;
+// launch-timestamp slots per timed call: FLL, FIR, loop kernel (start, end)
+// and one spare pair; qpsk_demod_enable_timing records the first kKtCalls calls
+constexpr int kKtPerCall = 8;
+constexpr int kKtCalls = 4096;
 constexpr int64_t kMaxSamplesPerCall = int64_t(1) << 30;
 // the symbol loop keeps sample indices of one call in 32-bit integers
 constexpr int64_t kMaxCallSamples = (int64_t(1) << 31) - 129;
@@ -125,11 +130,12 @@ struct qpsk_demod {
     float *d_xsyms = nullptr;
     size_t xsyms_bytes = 0;
     bool timing = false;
-    // one set of kEv events per timed call (start, FLL end, FIR start, FIR end,
-    // loop start, loop end), each on the stream its stage runs on; averaged by
-    // qpsk_demod_stage_times()
-    std::vector<std::array<hipEvent_t, kEv>> ev_pool;
-    size_t ev_used = 0;
+    // launch timestamps of the timed calls ([call][kKtPerCall] wall-clock ticks,
+    // written by the kernels themselves: qpsk_kernels.h kt_start / kt_end)
+    unsigned long long *d_kt = nullptr;
+    int kt_used = 0;
+    int wall_khz = 100000;
+    int cus = 0;
     // ---- pipelined calls (qpsk_demod_process_async) ----------------------
     bool pipe_ready = false;
     int pipe_bufs = 0;               // 2 = double-buffered stage boundary, 1 = no room for it
@@ -138,11 +144,13 @@ struct qpsk_demod {
     hipEvent_t e_in = nullptr;
     hipEvent_t e_front[2] = {nullptr, nullptr}, e_back[2] = {nullptr, nullptr};
     bool front_rec[2] = {false, false}, back_rec[2] = {false, false};
-    // FLL off: recorded on the back stream between the carry kernel and the
-    // loop kernel; the next call's FIR waits for it, so the loop kernel is
-    // dispatched first (see process_async_one)
-    hipEvent_t e_carry[2] = {nullptr, nullptr};
-    bool carry_rec[2] = {false, false};
+    // FLL off: residency counter (signal memory) the loop kernel's workgroups
+    // increment as they start; the next call's FIR waits for it to reach
+    // resident_gate (see process_async_one)
+    unsigned long long *d_resident = nullptr;
+    uint64_t resident_issued = 0;    // workgroups of every gated loop launch so far
+    uint64_t resident_gate = 0;      // what the newest gated loop launch brings it to, at least
+    bool gate_pending = false;       // the next FIR has a loop launch to wait for
     int last_back = -1;              // boundary buffer of the newest back stage, -1 = none
     int64_t *h_len[2] = {nullptr, nullptr};   // pinned staging of per-call lengths
 };
@@ -233,30 +241,15 @@ int validate(qpsk_demod *h, Call &c) {
     return QPSK_OK;
 }
 
-hipEvent_t *next_events(qpsk_demod *h, int *rc) {
-    *rc = QPSK_OK;
-    if (!h->timing) return nullptr;
-    if (h->ev_used == h->ev_pool.size()) {
-        std::array<hipEvent_t, kEv> set{};
-        for (auto &e : set) {
-            if (hipEventCreate(&e) != hipSuccess) {
-                *rc = fail(QPSK_ERR_DEVICE, "hipEventCreate");
-                return nullptr;
-            }
-        }
-        h->ev_pool.push_back(set);
-    }
-    return h->ev_pool[h->ev_used++].data();
+// the launch-timestamp slots of the next timed call, or nullptr
+unsigned long long *next_kt(qpsk_demod *h) {
+    if (!h->timing || !h->d_kt || h->kt_used >= kKtCalls) return nullptr;
+    return h->d_kt + static_cast<size_t>(kKtPerCall) * h->kt_used++;
 }
 
 }  // namespace (validation)
 
 namespace {
-
-#define EV(i, st)                                      \
-    do {                                               \
-        if (ev) HIP_TRY(hipEventRecord(ev[i], (st)));  \
-    } while (0)
 
 // optional IQ_Balancer pre-stage (IQ Balancer.cs:15-25) into d_iqb
 void run_iqb(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_len, int64_t n_call,
@@ -271,41 +264,41 @@ void run_iqb(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_l
 
 // FLL (Band-Edge Filter.cs:64-87), README order FLL -> MF
 void run_fll(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_len, int64_t n_call,
-             float *y, hipStream_t st) {
+             float *y, hipStream_t st, unsigned long long *kt) {
     FllArgs fa{};
     fa.x = x; fa.x_stride = x_stride;
     fa.y = y; fa.y_stride = h->n_max;
     fa.delay = h->d_fll_delay;
     fa.lengths = d_len; fa.n = n_call;
     fa.state = h->d_state; fa.S = h->S;
+    fa.kt = kt ? kt + 0 : nullptr;
     launch_fll(fa, h->fp, st);
 }
 
 // matched filter (QPSKDeModulator.cs:360) + FIR delay-line carry
 int run_fir(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_len, int64_t n_call,
-            float *mf, hipStream_t st, hipEvent_t *ev) {
+            float *mf, hipStream_t st, unsigned long long *kt) {
     FirArgs fa{};
     fa.x = x; fa.x_stride = x_stride;
     fa.hist = h->d_hist[h->hist_cur];
     fa.lengths = d_len; fa.n = n_call;
     fa.y = mf; fa.y_stride = h->mf_stride; fa.y_offset = kMfPrefix;
-    EV(2, st);
+    fa.kt = kt ? kt + 2 : nullptr;
     if (n_call > 0) {
         launch_fir(fa, h->d_hrev, h->T, h->W, h->S, n_call, st);
-        EV(3, st);
+        fa.kt = nullptr;
         launch_fir_hist(fa, h->d_hist[h->hist_cur ^ 1], h->T - 1, h->S, st);
         h->hist_cur ^= 1;
-    } else {
-        EV(3, st);
     }
     return QPSK_OK;
 }
 
 // symbol sync + Costas + decode (QPSKDeModulator.cs:364-408) and the output copies
+// resident: the pipelined path's residency counter (nullptr otherwise); the
+// launch's workgroup count is added to h->resident_issued
 int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipStream_t st,
-             hipEvent_t *ev, hipEvent_t after_carry = nullptr) {
+             unsigned long long *kt, unsigned long long *resident = nullptr) {
     const int S = h->S;
-    EV(4, st);
     LoopArgs la{};
     la.mf = mf; la.mf_stride = h->mf_stride;
     la.carry = h->d_carry;
@@ -320,11 +313,23 @@ int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipS
     la.syms_cap = h->syms_cap;
     la.n_syms = h->d_counts + S;
     la.S = S;
-    la.flags = h->d_flags + (c.mem == QPSK_MEM_HOST && !c.append ? 1 : 0);
+    // host-memory calls (chunks of one included) raise into slot 1, which the
+    // call clears first and reads back at its end; device-memory calls into
+    // slot 0, read by qpsk_demod_status
+    la.flags = h->d_flags + (c.mem == QPSK_MEM_HOST ? 1 : 0);
     la.chunked = c.append ? 1 : 0;
-    launch_loop(la, h->lp, c.mode, h->loop_variant, st, after_carry);
+    la.kt = kt ? kt + 4 : nullptr;
+    la.resident = resident;
+    const int grid = launch_loop(la, h->lp, c.mode, h->loop_variant, st);
     HIP_TRY(hipGetLastError());
-    EV(5, st);
+    if (resident) {
+        // the next FIR may start once min(grid, CUs) workgroups hold their CUs:
+        // at most one 104-147 KB loop workgroup fits a CU, and those are the
+        // first ones dispatched (never more than there are)
+        h->resident_gate = h->resident_issued + static_cast<uint64_t>(std::min(grid, std::max(h->cus, 1)));
+        h->resident_issued += static_cast<uint64_t>(grid);
+        h->gate_pending = true;
+    }
     if (c.append) {
         AppendArgs aa{};
         aa.dst_bits = c.mode == QPSK_MODE_DEMODULATE ? c.dst_bits : nullptr;
@@ -389,8 +394,12 @@ int pipe_setup(qpsk_demod *h) {
     for (int b = 0; b < 2; ++b) {
         HIP_TRY(hipEventCreateWithFlags(&h->e_front[b], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&h->e_back[b], hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&h->e_carry[b], hipEventDisableTiming));
         HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h->h_len[b]), h->S * sizeof(int64_t)));
+    }
+    if (!h->p.enable_fll) {
+        HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void **>(&h->d_resident), sizeof(unsigned long long),
+                                      hipMallocSignalMemory));
+        HIP_TRY(hipMemset(h->d_resident, 0, sizeof(unsigned long long)));
     }
     int rc;
     if (!h->d_lengths[1] && (rc = dev_alloc(&h->d_lengths[1], h->S))) return rc;
@@ -524,12 +533,13 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
     // Above half the CUs, too: no FIR workgroup fits beside a 147 KB one, and
     // pipelined calls then wait for the FIR (4096 streams: 37.7 vs 33.4 ms a
     // call; 2048: 24.6 vs 29.1 ms, profiles/r02_loop_shapes_c4_ab.txt)
-    if (h->loop_variant == 0 && h->lp.sps >= 8.0) {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) == hipSuccess &&
-            (h->S + 23) / 24 <= cus / 2)
-            h->loop_variant = 4;
-    }
+    if (hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess)
+        h->cus = 0;
+    if (hipDeviceGetAttribute(&h->wall_khz, hipDeviceAttributeWallClockRate, p->device) != hipSuccess ||
+        h->wall_khz <= 0)
+        h->wall_khz = 100000;
+    if (h->loop_variant == 0 && h->lp.sps >= 8.0 && h->cus > 0 && (h->S + 23) / 24 <= h->cus / 2)
+        h->loop_variant = 4;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipStreamCreate failed"));
     h->own_stream = true;
@@ -591,8 +601,9 @@ int qpsk_demod_destroy(qpsk_demod *h) {
         if (h->h_len[b]) hipHostFree(h->h_len[b]);
         if (h->e_front[b]) hipEventDestroy(h->e_front[b]);
         if (h->e_back[b]) hipEventDestroy(h->e_back[b]);
-        if (h->e_carry[b]) hipEventDestroy(h->e_carry[b]);
     }
+    if (h->d_resident) hipFree(h->d_resident);
+    hipFree(h->d_kt);
     hipFree(h->d_carry);
     hipFree(h->d_iqb);
     hipFree(h->d_state);
@@ -606,8 +617,6 @@ int qpsk_demod_destroy(qpsk_demod *h) {
     hipFree(h->d_acc);
     hipFree(h->d_xbits);
     hipFree(h->d_xsyms);
-    for (auto &set : h->ev_pool)
-        for (auto &e : set) hipEventDestroy(e);
     if (h->e_in) hipEventDestroy(h->e_in);
     if (h->s_front) hipStreamDestroy(h->s_front);
     if (h->s_back) hipStreamDestroy(h->s_back);
@@ -634,25 +643,77 @@ int qpsk_demod_set_stream(qpsk_demod *h, void *hip_stream) {
 
 int qpsk_demod_enable_timing(qpsk_demod *h, int32_t on) {
     if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
+    h->kt_used = 0;
     h->timing = on != 0;
-    h->ev_used = 0;
+    if (!h->timing) return QPSK_OK;
+    HIP_TRY(hipSetDevice(h->p.device));
+    int rc;
+    const size_t n = static_cast<size_t>(kKtCalls) * kKtPerCall;
+    if (!h->d_kt && (rc = dev_alloc(&h->d_kt, n))) return rc;
+    // (start, end) pairs: start = +inf for the atomic minimum, end = 0 for the maximum
+    std::vector<unsigned long long> init(n, 0ull);
+    for (size_t i = 0; i < n; i += 2) init[i] = ~0ull;
+    if ((rc = drain_async(h))) return rc;
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipMemcpy(h->d_kt, init.data(), n * sizeof(unsigned long long), hipMemcpyHostToDevice));
     return QPSK_OK;
 }
 
-int qpsk_demod_stage_times(const qpsk_demod *h, float *ms, int32_t n) {
-    if (!h || !ms) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
-    float sum[4] = {0, 0, 0, 0};
-    for (size_t c = 0; c < h->ev_used; ++c) HIP_TRY(hipEventSynchronize(h->ev_pool[c][kEv - 1]));
-    for (size_t c = 0; c < h->ev_used; ++c) {
-        const auto &e = h->ev_pool[c];
-        float t;
-        HIP_TRY(hipEventElapsedTime(&t, e[0], e[1])); sum[0] += t;
-        HIP_TRY(hipEventElapsedTime(&t, e[2], e[3])); sum[1] += t;
-        HIP_TRY(hipEventElapsedTime(&t, e[4], e[5])); sum[2] += t;
-        HIP_TRY(hipEventElapsedTime(&t, e[0], e[5])); sum[3] += t;
+// per timed call: FLL, FIR and loop kernel durations and the call's kernel
+// span (earliest start to latest end), ms; 0 for a kernel that did not run
+static int read_launch_times(qpsk_demod *h, std::vector<float> *out) {
+    out->assign(static_cast<size_t>(h->kt_used) * 4, 0.f);
+    if (!h->kt_used) return QPSK_OK;
+    int rc;
+    if ((rc = drain_async(h))) return rc;
+    HIP_TRY(hipSetDevice(h->p.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (h->s_front) HIP_TRY(hipStreamSynchronize(h->s_front));
+    if (h->s_back) HIP_TRY(hipStreamSynchronize(h->s_back));
+    std::vector<unsigned long long> t(static_cast<size_t>(h->kt_used) * kKtPerCall);
+    HIP_TRY(hipMemcpy(t.data(), h->d_kt, t.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    const double ms_per_tick = 1.0 / h->wall_khz;
+    for (int c = 0; c < h->kt_used; ++c) {
+        const unsigned long long *k = t.data() + static_cast<size_t>(kKtPerCall) * c;
+        unsigned long long lo = ~0ull, hi = 0;
+        for (int j = 0; j < 3; ++j) {
+            const unsigned long long s0 = k[2 * j], e0 = k[2 * j + 1];
+            if (s0 == ~0ull || e0 < s0) continue;   // did not run
+            (*out)[4 * c + j] = static_cast<float>((e0 - s0) * ms_per_tick);
+            lo = std::min(lo, s0);
+            hi = std::max(hi, e0);
+        }
+        if (hi >= lo && lo != ~0ull) (*out)[4 * c + 3] = static_cast<float>((hi - lo) * ms_per_tick);
     }
+    return QPSK_OK;
+}
+
+int qpsk_demod_stage_times(qpsk_demod *h, float *ms, int32_t n) {
+    if (!h || !ms) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    std::vector<float> t;
+    int rc;
+    if ((rc = read_launch_times(h, &t))) return rc;
     const int k = std::min<int32_t>(n, 4);
-    for (int i = 0; i < k; ++i) ms[i] = h->ev_used ? sum[i] / h->ev_used : 0.f;
+    for (int i = 0; i < k; ++i) {
+        double sum = 0;
+        int cnt = 0;
+        for (int c = 0; c < h->kt_used; ++c)
+            if (t[4 * c + i] > 0.f) {
+                sum += t[4 * c + i];
+                ++cnt;
+            }
+        ms[i] = cnt ? static_cast<float>(sum / cnt) : 0.f;
+    }
+    return k;
+}
+
+int qpsk_demod_launch_times(qpsk_demod *h, float *ms, int32_t max_calls) {
+    if (!h || !ms) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    std::vector<float> t;
+    int rc;
+    if ((rc = read_launch_times(h, &t))) return rc;
+    const int k = std::min<int32_t>(max_calls, h->kt_used);
+    std::memcpy(ms, t.data(), static_cast<size_t>(k) * 4 * sizeof(float));
     return k;
 }
 
@@ -673,9 +734,7 @@ int process_one(qpsk_demod *h, const Call &c) {
     HIP_TRY(hipSetDevice(h->p.device));
     // pipelined calls issued before this one finish first (they share the state)
     if (hipEvent_t e = last_async(h)) HIP_TRY(hipStreamWaitEvent(st, e, 0));
-    hipEvent_t *ev = next_events(h, &rc);
-    if (rc) return rc;
-    EV(0, st);
+    unsigned long long *kt = next_kt(h);
     if (mem == QPSK_MEM_HOST && !c.append) HIP_TRY(hipMemsetAsync(h->d_flags + 1, 0, sizeof(uint32_t), st));
 
     // ---- input -----------------------------------------------------------
@@ -700,13 +759,12 @@ int process_one(qpsk_demod *h, const Call &c) {
         x_stride = h->n_max;
     }
     if (h->p.enable_fll && n_call > 0) {
-        run_fll(h, x, x_stride, d_len, n_call, h->d_fll_out[0], st);
+        run_fll(h, x, x_stride, d_len, n_call, h->d_fll_out[0], st, kt);
         x = h->d_fll_out[0];
         x_stride = h->n_max;
     }
-    EV(1, st);
-    if ((rc = run_fir(h, x, x_stride, d_len, n_call, h->d_mf[0], st, ev))) return rc;
-    return run_loop(h, c, d_len, h->d_mf[0], st, ev);
+    if ((rc = run_fir(h, x, x_stride, d_len, n_call, h->d_mf[0], st, kt))) return rc;
+    return run_loop(h, c, d_len, h->d_mf[0], st, kt);
 }
 
 int process_async_one(qpsk_demod *h, const Call &c) {
@@ -729,8 +787,7 @@ int process_async_one(qpsk_demod *h, const Call &c) {
     HIP_TRY(hipStreamWaitEvent(F, h->e_in, 0));
     const int prev = h->pipe_bufs == 2 ? b : h->last_back;
     if (prev >= 0 && h->back_rec[prev]) HIP_TRY(hipStreamWaitEvent(F, h->e_back[prev], 0));
-    hipEvent_t *ev = next_events(h, &rc);
-    if (rc) return rc;
+    unsigned long long *kt = next_kt(h);
     const int64_t *d_len = nullptr;
     if (lengths) {
         // pinned staging row b is free once the front stage that last read it ran
@@ -739,7 +796,6 @@ int process_async_one(qpsk_demod *h, const Call &c) {
         HIP_TRY(hipMemcpyAsync(h->d_lengths[b], h->h_len[b], S * sizeof(int64_t), hipMemcpyHostToDevice, F));
         d_len = h->d_lengths[b];
     }
-    EV(0, F);
     const float *x = iq;
     int64_t x_stride = stride_floats / 2;
     if (h->p.iq_balance && n_call > 0) {
@@ -751,36 +807,38 @@ int process_async_one(qpsk_demod *h, const Call &c) {
     float *mf;
     if (h->p.enable_fll) {
         // front = FLL into boundary rows b; back = FIR (MF rows 0) + loop
-        if (n_call > 0) run_fll(h, x, x_stride, d_len, n_call, h->d_fll_out[b], F);
-        EV(1, F);
+        if (n_call > 0) run_fll(h, x, x_stride, d_len, n_call, h->d_fll_out[b], F, kt);
         HIP_TRY(hipEventRecord(h->e_front[b], F));
         HIP_TRY(hipStreamWaitEvent(B, h->e_front[b], 0));
         mf = h->d_mf[0];
         if ((rc = run_fir(h, n_call > 0 ? h->d_fll_out[b] : x, n_call > 0 ? h->n_max : x_stride, d_len,
-                          n_call, mf, B, ev)))
+                          n_call, mf, B, kt)))
             return rc;
     } else {
         // front = FIR into MF rows b; back = loop.  FIR(k+1) and loop(k) both
         // become ready when a stage of call k-1 or k ends, and whichever is
         // dispatched first takes the CUs: a loop kernel dispatched after the
-        // FIR finds no CU with room for its 125 KB workgroups and runs after
-        // it (measured on MI355X at C3 under rocprofv3: FIR 42 + loop 80 ms a
-        // call, against FIR 52 || loop 43 the other way round,
-        // profiles/r02_c3_dispatch_race.txt), and either order then repeats
-        // itself call after call.  So FIR(k+1)
-        // also waits for the carry kernel that precedes loop(k) on the back
-        // stream: the loop kernel is dispatched as that event signals.
-        if (h->last_back >= 0 && h->carry_rec[h->last_back])
-            HIP_TRY(hipStreamWaitEvent(F, h->e_carry[h->last_back], 0));
-        EV(1, F);
+        // FIR finds no CU with room for its 104-147 KB workgroups and runs
+        // after it (measured on MI355X at C3 under rocprofv3: FIR 42 + loop
+        // 80 ms a call, against FIR 52 || loop 43 the other way round,
+        // profiles/r02_c3_dispatch_race.txt; reproduced by
+        // tools/anyorder_probe.hip), and either order then repeats call after
+        // call.  So FIR(k+1) waits, on the device, until loop(k)'s workgroups
+        // hold their CUs: each adds 1 to the residency counter as it starts,
+        // and the front stream waits for the count (hipStreamWaitValue64 on
+        // signal memory).  The order no longer depends on dispatch timing:
+        // the FIR cannot be dispatched before min(grid, CUs) loop workgroups
+        // run, and every one of those was dispatched before it.
+        if (h->gate_pending)
+            HIP_TRY(hipStreamWaitValue64(F, h->d_resident, h->resident_gate, hipStreamWaitValueGte));
+        h->gate_pending = false;
         mf = h->d_mf[b];
-        if ((rc = run_fir(h, x, x_stride, d_len, n_call, mf, F, ev))) return rc;
+        if ((rc = run_fir(h, x, x_stride, d_len, n_call, mf, F, kt))) return rc;
         HIP_TRY(hipEventRecord(h->e_front[b], F));
         HIP_TRY(hipStreamWaitEvent(B, h->e_front[b], 0));
     }
     h->front_rec[b] = true;
-    if ((rc = run_loop(h, c, d_len, mf, B, ev, h->p.enable_fll ? nullptr : h->e_carry[b]))) return rc;
-    h->carry_rec[b] = !h->p.enable_fll;
+    if ((rc = run_loop(h, c, d_len, mf, B, kt, h->p.enable_fll ? nullptr : h->d_resident))) return rc;
     HIP_TRY(hipEventRecord(h->e_back[b], B));
     h->back_rec[b] = true;
     h->last_back = b;
@@ -875,7 +933,16 @@ int process_chunked(qpsk_demod *h, const Call &c, bool async) {
         sub.dst_syms_stride = dsyms_stride;
         sub.dst_n_bits = host ? nullptr : c.n_bits;
         sub.dst_n_syms = host ? nullptr : c.n_syms;
-        if ((rc = async ? process_async_one(h, sub) : process_one(h, sub))) return rc;
+        if ((rc = async ? process_async_one(h, sub) : process_one(h, sub))) {
+            // a chunk after the first failed: the chunks that ran left
+            // StreamState.tofs (the queue offset inside this call) non-zero,
+            // which only the last chunk resets; clear it so the next call's
+            // timing runs from its own queue start (best effort after a HIP error)
+            if (k > 0)
+                (void)hipMemset2DAsync(reinterpret_cast<char *>(h->d_state) + offsetof(StreamState, tofs),
+                                       sizeof(StreamState), 0, sizeof(int64_t), S, h->stream);
+            return rc;
+        }
     }
     if (!host) return QPSK_OK;
     hipStream_t st = h->stream;

@@ -170,6 +170,7 @@ def lib():
     L.qpsk_tsc_find.restype = C.c_int64
     L.qpsk_demod_enable_timing.argtypes = [C.c_void_p, C.c_int32]
     L.qpsk_demod_stage_times.argtypes = [C.c_void_p, _f32p, C.c_int32]
+    L.qpsk_demod_launch_times.argtypes = [C.c_void_p, _f32p, C.c_int32]
     L.qpsk_demod_rrc_taps.argtypes = [C.c_void_p, _f32p, C.c_int32]
     L.qpsk_demod_gains.argtypes = [C.c_void_p] + [_f64p] * 5
     L.qpsk_demod_fll_taps.argtypes = [C.c_void_p, _f32p, _f32p, C.c_int32]
@@ -210,7 +211,8 @@ def lib():
 EXPORTED_SYMBOLS = [
     "qpsk_abi_version", "qpsk_last_error", "qpsk_demod_params_init", "qpsk_demod_create",
     "qpsk_demod_destroy", "qpsk_demod_set_stream", "qpsk_demod_process", "qpsk_demod_max_symbols",
-    "qpsk_tsc_find", "qpsk_demod_enable_timing", "qpsk_demod_stage_times", "qpsk_demod_rrc_taps",
+    "qpsk_tsc_find", "qpsk_demod_enable_timing", "qpsk_demod_stage_times", "qpsk_demod_launch_times",
+    "qpsk_demod_rrc_taps",
     "qpsk_demod_gains", "qpsk_demod_fll_taps", "qpsk_demod_state_bytes", "qpsk_demod_get_state",
     "qpsk_demod_set_state", "qpsk_demod_design", "qpsk_framer_create", "qpsk_framer_destroy",
     "qpsk_framer_set_markers", "qpsk_framer_push", "qpsk_framer_dev_create",
@@ -304,9 +306,18 @@ class BatchDemodulator:
         _check(lib().qpsk_demod_enable_timing(self._h, 1 if on else 0))
 
     def stage_times(self):
+        """Average kernel launch times (ms) of the calls since enable_timing:
+        the kernels' own first-workgroup-start to last-workgroup-end spans."""
         ms = (C.c_float * 4)()
-        lib().qpsk_demod_stage_times(self._h, ms, 4)
+        _check(lib().qpsk_demod_stage_times(self._h, ms, 4))
         return {"fll": ms[0], "fir": ms[1], "loop": ms[2], "total": ms[3]}
+
+    def launch_times(self, max_calls=4096) -> np.ndarray:
+        """[calls, 4] float32: FLL, FIR, loop kernel and the call's kernel span
+        (ms) per call since enable_timing; 0 = the kernel did not run."""
+        out = np.zeros((max_calls, 4), dtype=np.float32)
+        k = _check(lib().qpsk_demod_launch_times(self._h, out.ctypes.data_as(_f32p), max_calls))
+        return out[:k].copy()
 
     def rrc_taps(self):
         out = np.zeros(4096, dtype=np.float32)

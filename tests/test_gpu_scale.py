@@ -285,3 +285,28 @@ def test_iq_balance_prestage_bit_exact(fll):
     from test_gpu_parity import async_run
     got_async, _ = async_run(iq, calls, 8, 8, iq_balance=True, **kw)
     assert_same(got_async, ref)
+
+
+def test_chunked_host_call_reports_nonfinite():
+    """A host-memory call longer than max_samples_per_call runs as internal
+    chunks; a NaN reaching the timing loop in any chunk fails the call with
+    the same error as an unchunked call (QPSK_ERR_STATE, 'non-finite'), and the
+    handle's status keeps the flag until read."""
+    S = 2
+    iq = K.batch_signals(S, seed0=690, sps=8, span=8, n_bits=1500, snr_db=18)
+    n = iq.shape[1] // 2
+    cap = n // 3
+    iq[1, 2 * (cap + 100)] = np.nan          # inside the second chunk
+    b = Q.BatchDemodulator(S, Q.params(K.FS, K.FS // 8, K.ALPHA, 8, max_samples_per_call=cap))
+    with pytest.raises(Q.QPSKError, match="non-finite"):
+        b.process(iq)
+    assert b.status() & Q.STATUS_NONFINITE_TIMING
+    assert b.status() == 0
+    # a clean call afterwards on a fresh handle state succeeds and matches the oracle
+    b.close()
+    clean = K.batch_signals(S, seed0=691, sps=8, span=8, n_bits=1500, snr_db=18)
+    b = Q.BatchDemodulator(S, Q.params(K.FS, K.FS // 8, K.ALPHA, 8, max_samples_per_call=cap))
+    bits, nb, _, _ = b.process(clean)
+    for s in range(S):
+        assert Q.unpack_bits(bits[s], int(nb[s])) == K.oracle_for(8, 8).DeModulate(clean[s])
+    b.close()
