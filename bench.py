@@ -538,7 +538,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
                     esn0_db=20.0 if cfg["impaired"] else None, device=dev.index)
     iq, tx = Q.synth_generate(S, n, FS, rs, first_stream=lo, **synth_kw)
     p = Q.params(FS, rs, ALPHA, span, enable_fll=cfg["fll"], device=dev.index, max_samples_per_call=n,
-                 loop_variant=args.loop_variant)
+                 loop_variant=args.loop_variant, costas_trig=args.costas_trig)
     demod = Q.BatchDemodulator(S, p)
     fresh_state = demod.get_state()   # for the parity / BER call (no second handle: C5 needs ~256 GiB)
     # a real stream (torch's legacy default is handle 0, which the C ABI reads
@@ -657,6 +657,8 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
         "config": {"workload": cfg["name"], "streams_per_gpu": S, "samples_per_stream": n,
                    "sps": sps, "taps": span * sps + 1, "fll": cfg["fll"],
                    "parallelism": f"stream-shard x{world}",
+                   "costas_trig": "glibc sin/cos (bit-exact)" if args.costas_trig else
+                                  "portable table sincos (<= 1 ulp from glibc)",
                    "calls": "serial" if args.serial_calls else
                             f"pipelined (front/back stage overlap, depth {demod.pipeline_depth()})"},
         "roofline": roof,
@@ -750,6 +752,8 @@ def main():
     ap.add_argument("--loop-variant", type=int, default=0,
                     help="symbol-loop kernel shape (qpsk_demod_params.loop_variant; 0 = auto)")
     ap.add_argument("--streams", type=int, default=0, help="override streams per GPU")
+    ap.add_argument("--costas-trig", type=int, default=0, choices=[0, 1],
+                    help="qpsk_demod_params.costas_trig: 0 portable table sincos, 1 glibc's own sin/cos")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="default: os.cpu_count()")

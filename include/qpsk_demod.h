@@ -84,7 +84,12 @@ typedef struct qpsk_demod_params {
                                        sample before the FLL / matched filter; 0 (default) =
                                        the reference DeModulate, which constructs the balancer
                                        (QPSKDeModulator.cs:38) but never calls it */
-    int32_t reserved[6];
+    int32_t costas_trig;            /* the Costas NCO's Math.Cos / Math.Sin (CostasLoopQpsk.cs:69-70):
+                                       0 (default) = a portable table sincos within 1 ulp of
+                                       glibc (bit-identical on ~98.7 % of arguments); 1 = glibc's
+                                       own sin / cos restated exactly (what .NET calls on Linux
+                                       x86-64; symbols bit-identical by construction, slower) */
+    int32_t reserved[5];
 } qpsk_demod_params;
 
 typedef struct qpsk_demod qpsk_demod;

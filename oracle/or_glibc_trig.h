@@ -1,0 +1,261 @@
+/*
+ * or_glibc_trig.h -- ORACLE (test infrastructure only) restatement of glibc's
+ * double sin and cos, the functions .NET's Math.Sin / Math.Cos call on a Linux
+ * x86-64 host (the Costas loop's NCO, CostasLoopQpsk.cs:69-70).  The product
+ * keeps its own copy (qpsk-modulator-demodulator_amd/csrc/qpsk_glibc_trig.h);
+ * tests/test_oracle.py requires the two to agree and both to equal the real
+ * libm sin/cos (tools/check_glibc_sin.c).
+ *
+ * glibc 2.35 sysdeps/ieee754/dbl-64/s_sin.c, as its x86-64 FMA ifunc variant
+ * (s_sin-fma.c: the same source built with -mfma -mavx2, selected on every
+ * AVX2 + FMA host, the GPU boxes' EPYC hosts included) evaluates it: gcc
+ * contracts every a*b +- c whose product has no other use into one fma, and
+ * the fma() calls below are exactly those (read off the variant's code in
+ * this image's libm.so.6).  __branred (branred.c, Payne-Hanek for |x| >=
+ * 105414350) is the generic build, no fma.  Tables: or_glibc_tables.h
+ * (tools/gen_glibc_trig_tables.py).
+ *
+ *   |x| < 2^-26 (sin) / 2^-27 (cos)   x / 1.0
+ *   |x| < 0.855469                    do_sin(x, 0) / do_cos(x, 0)
+ *   |x| < 2.426265                    via pi/2 - |x| (two-part pi/2)
+ *   |x| < 105414350                   x - n pi/2 in three parts (reduce_sincos)
+ *   finite                            __branred
+ *   Inf / NaN                         x / x
+ * do_sin / do_cos: table value at the nearest multiple of 1/128 plus a
+ * degree-5 correction; do_sin switches to a Taylor form below 0.126.
+ *
+ * Compile with -ffp-contract=off (the fma calls are explicit).
+ */
+#ifndef OR_GLIBC_TRIG_H
+#define OR_GLIBC_TRIG_H
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "or_glibc_tables.h"
+
+static const double or_gl_sincostab[440] = {QPSK_GLIBC_SINCOSTAB_VALUES};
+static const double or_gl_toverp[75] = {QPSK_GLIBC_TOVERP_VALUES};
+
+static inline uint64_t or_gl_bits(double x)
+{
+    uint64_t u;
+    memcpy(&u, &x, 8);
+    return u;
+}
+
+static inline double or_gl_from_bits(uint64_t u)
+{
+    double x;
+    memcpy(&x, &u, 8);
+    return x;
+}
+
+/* usncs.h / s_sin.c constants */
+#define OR_GL_S1 (-0x1.5555555555555p-3)
+#define OR_GL_S2 (0x1.1111111110ecep-7)
+#define OR_GL_S3 (-0x1.a01a019db08b8p-13)
+#define OR_GL_S4 (0x1.71de27b9a7ed9p-19)
+#define OR_GL_S5 (-0x1.addffc2fcdf59p-26)
+#define OR_GL_SN3 (-0x1.5555555555515p-3)
+#define OR_GL_SN5 (0x1.11110e829872fp-7)
+#define OR_GL_CS2 (0x1p-1)
+#define OR_GL_CS4 (-0x1.5555555555535p-5)
+#define OR_GL_CS6 (0x1.6c16bedd9e239p-10)
+#define OR_GL_BIG (0x1.8p45)
+#define OR_GL_HP0 (0x1.921fb54442d18p0)
+#define OR_GL_HP1 (0x1.1a62633145c07p-54)
+#define OR_GL_MP1 (0x1.921fb58p0)
+#define OR_GL_MP2 (-0x1.dde973cp-27)
+#define OR_GL_PP3 (-0x1.cb3b398p-55)
+#define OR_GL_PP4 (-0x1.d747f23e32ed7p-83)
+#define OR_GL_HPINV (0x1.45f306dc9c883p-1)
+#define OR_GL_TOINT (0x1.8p52)
+
+/* TAYLOR_SIN (s_sin.c): a + ((POLY(xx) * a - 0.5 * da) * xx + da) */
+static inline double or_gl_taylor_sin(double a, double da)
+{
+    const double xx = a * a;
+    double p = fma(xx, OR_GL_S5, OR_GL_S4);
+    p = fma(xx, p, OR_GL_S3);
+    p = fma(xx, p, OR_GL_S2);
+    p = fma(xx, p, OR_GL_S1);
+    const double t = fma(xx, fma(p, a, -(0.5 * da)), da);
+    return a + t;
+}
+
+/* table index of u = big + |x|: its low word, times 4 */
+static inline int or_gl_tab_index(double u)
+{
+    return (int)((uint32_t)or_gl_bits(u) << 2);
+}
+
+static inline double or_gl_do_cos(double x, double dx)
+{
+    if (x < 0) dx = -dx;
+    const double ax = fabs(x);
+    const double u = OR_GL_BIG + ax;
+    const double xr = (ax - (u - OR_GL_BIG)) + dx;
+    const double xx = xr * xr;
+    const double s = fma(xr * xx, fma(xx, OR_GL_SN5, OR_GL_SN3), xr);
+    const double c = xx * fma(xx, fma(xx, OR_GL_CS6, OR_GL_CS4), OR_GL_CS2);
+    const double *t = or_gl_sincostab + or_gl_tab_index(u);
+    const double sn = t[0], ssn = t[1], cs = t[2], ccs = t[3];
+    double cor = fma(-s, ssn, ccs);
+    cor = fma(-c, cs, cor);
+    cor = fma(-s, sn, cor);
+    return cs + cor;
+}
+
+static inline double or_gl_do_sin(double x, double dx)
+{
+    const double xold = x;
+    if (fabs(x) < 0.126) return or_gl_taylor_sin(x, dx);
+    if (x <= 0) dx = -dx;
+    const double ax = fabs(x);
+    const double u = OR_GL_BIG + ax;
+    const double xr = ax - (u - OR_GL_BIG);
+    const double xx = xr * xr;
+    const double s = xr + fma(xr * xx, fma(xx, OR_GL_SN5, OR_GL_SN3), dx);
+    const double c = fma(xr, dx, xx * fma(xx, fma(xx, OR_GL_CS6, OR_GL_CS4), OR_GL_CS2));
+    const double *t = or_gl_sincostab + or_gl_tab_index(u);
+    const double sn = t[0], ssn = t[1], cs = t[2], ccs = t[3];
+    double cor = fma(s, ccs, ssn);
+    cor = fma(-c, sn, cor);
+    cor = fma(s, cs, cor);
+    return copysign(sn + cor, xold);
+}
+
+/* x = n pi/2 + (a + da), |x| < 105414350 (s_sin.c reduce_sincos) */
+static inline int or_gl_reduce_sincos(double x, double *a, double *da)
+{
+    const double t = fma(x, OR_GL_HPINV, OR_GL_TOINT);
+    const double xn = t - OR_GL_TOINT;
+    double y = fma(-xn, OR_GL_MP1, x);
+    y = fma(-xn, OR_GL_MP2, y);
+    const int n = (int)(or_gl_bits(t) & 3);
+    const double t2 = fma(-xn, OR_GL_PP3, y);
+    double db = fma(-xn, OR_GL_PP3, y - t2);
+    const double b = fma(-xn, OR_GL_PP4, t2);
+    db = db + fma(-xn, OR_GL_PP4, t2 - b);
+    *a = b;
+    *da = db;
+    return n;
+}
+
+/* branred.c: one of the two halves of x (x1 / x2) against 2/pi */
+static inline void or_gl_branred_part(double xi, double *bo, double *bbo, double *sumo)
+{
+    const double big = 0x1.8p52, big1 = 0x1.8p54;
+    double r[6], s, t, sum = 0, b, bb;
+    int k = (int)((((int64_t)or_gl_bits(xi)) >> 52) & 2047);
+    k = (k - 450) / 24;
+    if (k < 0) k = 0;
+    double gor = or_gl_from_bits((uint64_t)(0x63f00000u - (uint32_t)((k * 24) << 20)) << 32);
+    for (int i = 0; i < 6; i++) {
+        r[i] = xi * or_gl_toverp[k + i] * gor;
+        gor *= 0x1p-24;
+    }
+    for (int i = 0; i < 3; i++) {
+        s = (r[i] + big) - big;
+        sum += s;
+        r[i] -= s;
+    }
+    t = 0;
+    for (int i = 0; i < 6; i++) t += r[5 - i];
+    bb = (((((r[0] - t) + r[1]) + r[2]) + r[3]) + r[4]) + r[5];
+    s = (t + big) - big;
+    sum += s;
+    t -= s;
+    b = t + bb;
+    bb = (t - b) + bb;
+    s = (sum + big1) - big1;
+    sum -= s;
+    *bo = b;
+    *bbo = bb;
+    *sumo = sum;
+}
+
+/* x = n pi/2 + (a + aa) for a finite |x| >= 105414350 (branred.c __branred) */
+static inline int or_gl_branred(double x, double *a, double *aa)
+{
+    const double split = 134217729.0, mp2 = -0x1.dde974p-27;
+    double b1, bb1, sum1, b2, bb2, sum2;
+    x *= 0x1p-600;
+    double t = x * split;
+    const double x1 = t - (t - x);
+    const double x2 = x - x1;
+    or_gl_branred_part(x1, &b1, &bb1, &sum1);
+    or_gl_branred_part(x2, &b2, &bb2, &sum2);
+    double sum = sum1 + sum2;
+    double b = b1 + b2;
+    double bb = (fabs(b1) > fabs(b2)) ? (b1 - b) + b2 : (b2 - b) + b1;
+    if (b > 0.5) {
+        b -= 1.0;
+        sum += 1.0;
+    } else if (b < -0.5) {
+        b += 1.0;
+        sum -= 1.0;
+    }
+    double s = b + (bb + bb1 + bb2);
+    t = ((b - s) + bb) + (bb1 + bb2);
+    b = s * split;
+    const double t1 = b - (b - s);
+    const double t2 = s - t1;
+    b = s * OR_GL_HP0;
+    bb = (((t1 * OR_GL_MP1 - b) + t1 * mp2) + t2 * OR_GL_MP1) + (t2 * mp2 + s * OR_GL_HP1 + t * OR_GL_HP0);
+    s = b + bb;
+    t = (b - s) + bb;
+    *a = s;
+    *aa = t;
+    return ((int)sum) & 3;
+}
+
+static inline double or_gl_do_sincos(double a, double da, int n)
+{
+    const double r = (n & 1) ? or_gl_do_cos(a, da) : or_gl_do_sin(a, da);
+    return (n & 2) ? -r : r;
+}
+
+static inline double or_glibc_sin(double x)
+{
+    const uint32_t k = (uint32_t)(or_gl_bits(x) >> 32) & 0x7fffffffu;
+    double a, da;
+    if (k < 0x3e500000u) return x;
+    if (k < 0x3feb6000u) return or_gl_do_sin(x, 0.0);
+    if (k < 0x400368fdu) return copysign(or_gl_do_cos(OR_GL_HP0 - fabs(x), OR_GL_HP1), x);
+    if (k < 0x419921fbu) {
+        const int n = or_gl_reduce_sincos(x, &a, &da);
+        return or_gl_do_sincos(a, da, n);
+    }
+    if (k < 0x7ff00000u) {
+        const int n = or_gl_branred(x, &a, &da);
+        return or_gl_do_sincos(a, da, n);
+    }
+    return x / x;
+}
+
+static inline double or_glibc_cos(double x)
+{
+    const uint32_t k = (uint32_t)(or_gl_bits(x) >> 32) & 0x7fffffffu;
+    double a, da;
+    if (k < 0x3e400000u) return 1.0;
+    if (k < 0x3feb6000u) return or_gl_do_cos(x, 0.0);
+    if (k < 0x400368fdu) {
+        const double y = OR_GL_HP0 - fabs(x);
+        a = y + OR_GL_HP1;
+        da = (y - a) + OR_GL_HP1;
+        return or_gl_do_sin(a, da);
+    }
+    if (k < 0x419921fbu) {
+        const int n = or_gl_reduce_sincos(x, &a, &da);
+        return or_gl_do_sincos(a, da, n + 1);
+    }
+    if (k < 0x7ff00000u) {
+        const int n = or_gl_branred(x, &a, &da);
+        return or_gl_do_sincos(a, da, n + 1);
+    }
+    return x / x;
+}
+
+#endif /* OR_GLIBC_TRIG_H */

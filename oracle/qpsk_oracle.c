@@ -32,14 +32,23 @@
 /* Math.Pow goes to the platform libm; keep gcc from folding pow(x, 2.0) into
  * x*x (glibc pow(x, 2.0) is not always the correctly rounded x*x). */
 static double (*volatile or_pow)(double, double) = pow;
+/* Math.Sin / Math.Cos (and the MathF pair) are separate libm calls in .NET;
+ * gcc would merge a sin and a cos of one argument into one sincos() call
+ * (its cse_sincos pass, no -ffast-math needed), and glibc's sincos is not
+ * bit-identical to sin (0.855 <= |x| < 2.426 reduces pi/2 - |x| differently).
+ * Calls through volatile pointers keep them separate, as .NET makes them. */
+static double (*volatile or_libm_sin)(double) = sin;
+static double (*volatile or_libm_cos)(double) = cos;
+static float (*volatile or_libm_sinf)(float) = sinf;
+static float (*volatile or_libm_cosf)(float) = cosf;
 
 static void trig_d(int mode, double x, double *s, double *c)
 {
     if (mode == OR_TRIG_PORTABLE) {
         or_sincos(x, s, c);
     } else {
-        *c = cos(x);
-        *s = sin(x);
+        *c = or_libm_cos(x);                 /* CostasLoopQpsk.cs:69 */
+        *s = or_libm_sin(x);                 /* :70 */
     }
 }
 
@@ -48,8 +57,8 @@ static void trig_f(int mode, float x, float *s, float *c)
     if (mode == OR_TRIG_PORTABLE) {
         or_sincosf(x, s, c);
     } else {
-        *c = cosf(x);
-        *s = sinf(x);
+        *c = or_libm_cosf(x);
+        *s = or_libm_sinf(x);
     }
 }
 
@@ -74,10 +83,10 @@ int or_rrc_taps(double span_symbols, double beta, int sample_rate, int symbol_ra
             val = 1.0 + beta * (4.0 / pi - 1.0);                /* :44 */
         } else if (fabs(fabs(t) - 1.0 / (4.0 * beta)) < eps) {
             val = (beta / sqrt(2.0)) *
-                  ((1.0 + 2.0 / pi) * sin(pi / (4.0 * beta)) +
-                   (1.0 - 2.0 / pi) * cos(pi / (4.0 * beta))); /* :49-51 */
+                  ((1.0 + 2.0 / pi) * or_libm_sin(pi / (4.0 * beta)) +
+                   (1.0 - 2.0 / pi) * or_libm_cos(pi / (4.0 * beta))); /* :49-51 */
         } else {
-            double num = sin(pi * t * (1.0 - beta)) + 4.0 * beta * t * cos(pi * t * (1.0 + beta));
+            double num = or_libm_sin(pi * t * (1.0 - beta)) + 4.0 * beta * t * or_libm_cos(pi * t * (1.0 + beta));
             double den = pi * t * (1.0 - or_pow(4.0 * beta * t, 2.0));
             val = num / den;                                    /* :56-59 */
         }
@@ -433,7 +442,7 @@ static float fll_sinc(float x)                                    /* :197-202 */
 {
     if (x == 0.0f) return 1.0f;
     float arg = OR_PI_F * x;
-    return sinf(arg) / arg;
+    return or_libm_sinf(arg) / arg;
 }
 
 or_fll *or_fll_new(float sps, float rolloff, int filter_size, float bandwidth, int lanes,
@@ -470,8 +479,8 @@ or_fll *or_fll_new(float sps, float rolloff, int filter_size, float bandwidth, i
     for (int i = 0; i < nt; i++) {
         float k = (float)(i - mid) / (2.0f * sps);
         float angle = -TWO_PI * (1.0f + rolloff) * k;
-        float wc = cosf(angle);
-        float ws = sinf(angle);
+        float wc = or_libm_cosf(angle);
+        float ws = or_libm_sinf(angle);
         float li = bb[i] * wc;
         float lq = bb[i] * ws;
         f->lower_iq[2 * i] = li; f->lower_iq[2 * i + 1] = lq;
@@ -1269,8 +1278,8 @@ void or_nco_next(or_nco *n, double *re, double *im)
     double inc = 2.0 * OR_PI * n->cur_hz / n->fs;
     n->phase += inc;
     nco_wrap(n);
-    *re = cos(n->phase);
-    *im = sin(n->phase);
+    *re = or_libm_cos(n->phase);
+    *im = or_libm_sin(n->phase);
 }
 
 void or_apply_lo_pair(or_nco *tx, or_nco *rx, float *iq, long n_complex)

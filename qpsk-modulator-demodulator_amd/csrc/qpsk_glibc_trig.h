@@ -1,0 +1,376 @@
+/*
+ * qpsk_glibc_trig.h -- PRODUCT restatement of glibc's double sin and cos, the
+ * functions .NET's Math.Sin / Math.Cos call on a Linux x86-64 host (the Costas
+ * loop's NCO, CostasLoopQpsk.cs:69-70), for qpsk_demod_params.costas_trig = 1.
+ *
+ * glibc 2.35 sysdeps/ieee754/dbl-64/s_sin.c as its x86-64 FMA ifunc variant
+ * evaluates it (every a*b +- c gcc contracts is an explicit fma here), with
+ * the generic __branred (branred.c, no fma) for |x| >= 105414350.  The oracle
+ * keeps its own copy (oracle/or_glibc_trig.h); tools/check_glibc_sin.c checks
+ * the oracle copy against the real libm (680M inputs: 0 differences) and
+ * tests/test_oracle.py checks this copy against the oracle's.
+ *
+ * Host + device.  The sincos table is passed in (the loop kernel stages it in
+ * LDS); toverp (Payne-Hanek, rare) is read from the constant copy.  Compile
+ * with -ffp-contract=off (the fma calls are explicit).
+ */
+#ifndef QPSK_GLIBC_TRIG_H
+#define QPSK_GLIBC_TRIG_H
+#include <math.h>
+#include <stdint.h>
+
+#include "qpsk_glibc_tables.h"
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define QPSK_GHD __host__ __device__
+#else
+#define QPSK_GHD
+#endif
+
+static const double qpsk_gl_sincostab_host[440] = {QPSK_GLIBC_SINCOSTAB_VALUES};
+#if defined(__HIPCC__)
+static __device__ const double qpsk_gl_sincostab_dev[440] = {QPSK_GLIBC_SINCOSTAB_VALUES};
+static __device__ const double qpsk_gl_toverp_dev[75] = {QPSK_GLIBC_TOVERP_VALUES};
+#endif
+static const double qpsk_gl_toverp_host[75] = {QPSK_GLIBC_TOVERP_VALUES};
+
+QPSK_GHD static inline const double *qpsk_gl_toverp(void)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return qpsk_gl_toverp_dev;
+#else
+    return qpsk_gl_toverp_host;
+#endif
+}
+
+QPSK_GHD static inline uint64_t qpsk_gl_bits(double x)
+{
+    union { double d; uint64_t u; } v;
+    v.d = x;
+    return v.u;
+}
+
+QPSK_GHD static inline double qpsk_gl_from_bits(uint64_t u)
+{
+    union { double d; uint64_t u; } v;
+    v.u = u;
+    return v.d;
+}
+
+/* usncs.h / s_sin.c constants */
+#define QPSK_GL_S1 (-0x1.5555555555555p-3)
+#define QPSK_GL_S2 (0x1.1111111110ecep-7)
+#define QPSK_GL_S3 (-0x1.a01a019db08b8p-13)
+#define QPSK_GL_S4 (0x1.71de27b9a7ed9p-19)
+#define QPSK_GL_S5 (-0x1.addffc2fcdf59p-26)
+#define QPSK_GL_SN3 (-0x1.5555555555515p-3)
+#define QPSK_GL_SN5 (0x1.11110e829872fp-7)
+#define QPSK_GL_CS2 (0x1p-1)
+#define QPSK_GL_CS4 (-0x1.5555555555535p-5)
+#define QPSK_GL_CS6 (0x1.6c16bedd9e239p-10)
+#define QPSK_GL_BIG (0x1.8p45)
+#define QPSK_GL_HP0 (0x1.921fb54442d18p0)
+#define QPSK_GL_HP1 (0x1.1a62633145c07p-54)
+#define QPSK_GL_MP1 (0x1.921fb58p0)
+#define QPSK_GL_MP2 (-0x1.dde973cp-27)
+#define QPSK_GL_PP3 (-0x1.cb3b398p-55)
+#define QPSK_GL_PP4 (-0x1.d747f23e32ed7p-83)
+#define QPSK_GL_HPINV (0x1.45f306dc9c883p-1)
+#define QPSK_GL_TOINT (0x1.8p52)
+
+/* TAYLOR_SIN (s_sin.c): a + ((POLY(xx) * a - 0.5 * da) * xx + da) */
+QPSK_GHD static inline double qpsk_gl_taylor_sin(double a, double da)
+{
+    const double xx = a * a;
+    double p = fma(xx, QPSK_GL_S5, QPSK_GL_S4);
+    p = fma(xx, p, QPSK_GL_S3);
+    p = fma(xx, p, QPSK_GL_S2);
+    p = fma(xx, p, QPSK_GL_S1);
+    const double t = fma(xx, fma(p, a, -(0.5 * da)), da);
+    return a + t;
+}
+
+/* table index of u = big + |x|: its low word, times 4 */
+QPSK_GHD static inline int qpsk_gl_tab_index(double u)
+{
+    return (int)((uint32_t)qpsk_gl_bits(u) << 2);
+}
+
+QPSK_GHD static inline double qpsk_gl_do_cos(double x, double dx, const double *tab)
+{
+    if (x < 0) dx = -dx;
+    const double ax = fabs(x);
+    const double u = QPSK_GL_BIG + ax;
+    const double xr = (ax - (u - QPSK_GL_BIG)) + dx;
+    const double xx = xr * xr;
+    const double s = fma(xr * xx, fma(xx, QPSK_GL_SN5, QPSK_GL_SN3), xr);
+    const double c = xx * fma(xx, fma(xx, QPSK_GL_CS6, QPSK_GL_CS4), QPSK_GL_CS2);
+    const double *t = tab + qpsk_gl_tab_index(u);
+    const double sn = t[0], ssn = t[1], cs = t[2], ccs = t[3];
+    double cor = fma(-s, ssn, ccs);
+    cor = fma(-c, cs, cor);
+    cor = fma(-s, sn, cor);
+    return cs + cor;
+}
+
+QPSK_GHD static inline double qpsk_gl_do_sin(double x, double dx, const double *tab)
+{
+    const double xold = x;
+    if (fabs(x) < 0.126) return qpsk_gl_taylor_sin(x, dx);
+    if (x <= 0) dx = -dx;
+    const double ax = fabs(x);
+    const double u = QPSK_GL_BIG + ax;
+    const double xr = ax - (u - QPSK_GL_BIG);
+    const double xx = xr * xr;
+    const double s = xr + fma(xr * xx, fma(xx, QPSK_GL_SN5, QPSK_GL_SN3), dx);
+    const double c = fma(xr, dx, xx * fma(xx, fma(xx, QPSK_GL_CS6, QPSK_GL_CS4), QPSK_GL_CS2));
+    const double *t = tab + qpsk_gl_tab_index(u);
+    const double sn = t[0], ssn = t[1], cs = t[2], ccs = t[3];
+    double cor = fma(s, ccs, ssn);
+    cor = fma(-c, sn, cor);
+    cor = fma(s, cs, cor);
+    return copysign(sn + cor, xold);
+}
+
+/* x = n pi/2 + (a + da), |x| < 105414350 (s_sin.c reduce_sincos) */
+QPSK_GHD static inline int qpsk_gl_reduce_sincos(double x, double *a, double *da)
+{
+    const double t = fma(x, QPSK_GL_HPINV, QPSK_GL_TOINT);
+    const double xn = t - QPSK_GL_TOINT;
+    double y = fma(-xn, QPSK_GL_MP1, x);
+    y = fma(-xn, QPSK_GL_MP2, y);
+    const int n = (int)(qpsk_gl_bits(t) & 3);
+    const double t2 = fma(-xn, QPSK_GL_PP3, y);
+    double db = fma(-xn, QPSK_GL_PP3, y - t2);
+    const double b = fma(-xn, QPSK_GL_PP4, t2);
+    db = db + fma(-xn, QPSK_GL_PP4, t2 - b);
+    *a = b;
+    *da = db;
+    return n;
+}
+
+/* branred.c: one of the two halves of x (x1 / x2) against 2/pi */
+QPSK_GHD static inline void qpsk_gl_branred_part(double xi, double *bo, double *bbo, double *sumo)
+{
+    const double big = 0x1.8p52, big1 = 0x1.8p54;
+    double r[6], s, t, sum = 0, b, bb;
+    const double *toverp = qpsk_gl_toverp();
+    int k = (int)((((int64_t)qpsk_gl_bits(xi)) >> 52) & 2047);
+    k = (k - 450) / 24;
+    if (k < 0) k = 0;
+    double gor = qpsk_gl_from_bits((uint64_t)(0x63f00000u - (uint32_t)((k * 24) << 20)) << 32);
+    for (int i = 0; i < 6; i++) {
+        r[i] = xi * toverp[k + i] * gor;
+        gor *= 0x1p-24;
+    }
+    for (int i = 0; i < 3; i++) {
+        s = (r[i] + big) - big;
+        sum += s;
+        r[i] -= s;
+    }
+    t = 0;
+    for (int i = 0; i < 6; i++) t += r[5 - i];
+    bb = (((((r[0] - t) + r[1]) + r[2]) + r[3]) + r[4]) + r[5];
+    s = (t + big) - big;
+    sum += s;
+    t -= s;
+    b = t + bb;
+    bb = (t - b) + bb;
+    s = (sum + big1) - big1;
+    sum -= s;
+    *bo = b;
+    *bbo = bb;
+    *sumo = sum;
+}
+
+/* x = n pi/2 + (a + aa) for a finite |x| >= 105414350 (branred.c __branred) */
+QPSK_GHD static inline int qpsk_gl_branred(double x, double *a, double *aa)
+{
+    const double split = 134217729.0, mp2 = -0x1.dde974p-27;
+    double b1, bb1, sum1, b2, bb2, sum2;
+    x *= 0x1p-600;
+    double t = x * split;
+    const double x1 = t - (t - x);
+    const double x2 = x - x1;
+    qpsk_gl_branred_part(x1, &b1, &bb1, &sum1);
+    qpsk_gl_branred_part(x2, &b2, &bb2, &sum2);
+    double sum = sum1 + sum2;
+    double b = b1 + b2;
+    double bb = (fabs(b1) > fabs(b2)) ? (b1 - b) + b2 : (b2 - b) + b1;
+    if (b > 0.5) {
+        b -= 1.0;
+        sum += 1.0;
+    } else if (b < -0.5) {
+        b += 1.0;
+        sum -= 1.0;
+    }
+    double s = b + (bb + bb1 + bb2);
+    t = ((b - s) + bb) + (bb1 + bb2);
+    b = s * split;
+    const double t1 = b - (b - s);
+    const double t2 = s - t1;
+    b = s * QPSK_GL_HP0;
+    bb = (((t1 * QPSK_GL_MP1 - b) + t1 * mp2) + t2 * QPSK_GL_MP1) + (t2 * mp2 + s * QPSK_GL_HP1 + t * QPSK_GL_HP0);
+    s = b + bb;
+    t = (b - s) + bb;
+    *a = s;
+    *aa = t;
+    return ((int)sum) & 3;
+}
+
+QPSK_GHD static inline double qpsk_gl_do_sincos(double a, double da, int n, const double *tab)
+{
+    const double r = (n & 1) ? qpsk_gl_do_cos(a, da, tab) : qpsk_gl_do_sin(a, da, tab);
+    return (n & 2) ? -r : r;
+}
+
+QPSK_GHD static inline double qpsk_glibc_sin(double x, const double *tab)
+{
+    const uint32_t k = (uint32_t)(qpsk_gl_bits(x) >> 32) & 0x7fffffffu;
+    double a, da;
+    if (k < 0x3e500000u) return x;
+    if (k < 0x3feb6000u) return qpsk_gl_do_sin(x, 0.0, tab);
+    if (k < 0x400368fdu) return copysign(qpsk_gl_do_cos(QPSK_GL_HP0 - fabs(x), QPSK_GL_HP1, tab), x);
+    if (k < 0x419921fbu) {
+        const int n = qpsk_gl_reduce_sincos(x, &a, &da);
+        return qpsk_gl_do_sincos(a, da, n, tab);
+    }
+    if (k < 0x7ff00000u) {
+        const int n = qpsk_gl_branred(x, &a, &da);
+        return qpsk_gl_do_sincos(a, da, n, tab);
+    }
+    return x / x;
+}
+
+QPSK_GHD static inline double qpsk_glibc_cos(double x, const double *tab)
+{
+    const uint32_t k = (uint32_t)(qpsk_gl_bits(x) >> 32) & 0x7fffffffu;
+    double a, da;
+    if (k < 0x3e400000u) return 1.0;
+    if (k < 0x3feb6000u) return qpsk_gl_do_cos(x, 0.0, tab);
+    if (k < 0x400368fdu) {
+        const double y = QPSK_GL_HP0 - fabs(x);
+        a = y + QPSK_GL_HP1;
+        da = (y - a) + QPSK_GL_HP1;
+        return qpsk_gl_do_sin(a, da, tab);
+    }
+    if (k < 0x419921fbu) {
+        const int n = qpsk_gl_reduce_sincos(x, &a, &da);
+        return qpsk_gl_do_sincos(a, da, n + 1, tab);
+    }
+    if (k < 0x7ff00000u) {
+        const int n = qpsk_gl_branred(x, &a, &da);
+        return qpsk_gl_do_sincos(a, da, n + 1, tab);
+    }
+    return x / x;
+}
+
+
+/* sin and cos of one argument (the Costas NCO needs both), as two calls */
+QPSK_GHD static inline void qpsk_glibc_sincos(double x, const double *tab, double *s, double *c)
+{
+    *s = qpsk_glibc_sin(x, tab);
+    *c = qpsk_glibc_cos(x, tab);
+}
+
+/* ---- branch-free form for wavefront code ---------------------------------
+ * glibc's sin(x) and cos(x) each pick an argument region and then evaluate
+ * one do_sin or do_cos; per region the pair needs exactly one do_sin and one
+ * do_cos:
+ *   |x| < 0.855469   sin = do_sin(x, 0)             cos = do_cos(x, 0)
+ *   |x| < 2.426265   sin = +-do_cos(y, hp1)         cos = do_sin(y + hp1, da)
+ *                    (y = hp0 - |x|)
+ *   otherwise        n, a, da = reduce_sincos / __branred: sin and cos are
+ *                    do_sin(a, da) and do_cos(a, da), swapped when n is odd,
+ *                    negated by bit 1 of n (sin) and of n + 1 (cos)
+ * so every lane evaluates one do_sin and one do_cos on selected arguments and
+ * the results are assigned by selects: one instruction stream for the whole
+ * wave instead of a branch per region and function.  Only __branred (|x| >=
+ * 105414350, a QPSK false lock) stays a branch.  Bit-identical to
+ * qpsk_glibc_sin / qpsk_glibc_cos (tools/check_glibc_sin.c -DWITH_PRODUCT). */
+QPSK_GHD static inline int qpsk_gl_tab_index_clamped(double u)
+{
+    /* valid arguments give i <= 109 (4 * 109 = 436); NaN / Inf any bits */
+    const uint32_t i = (uint32_t)qpsk_gl_bits(u) << 2;
+    return (int)(i < 436u ? i : 436u);
+}
+
+QPSK_GHD static inline double qpsk_gl_do_sin_bf(double x, double dx, const double *tab)
+{
+    const double ty = qpsk_gl_taylor_sin(x, dx);
+    const double dxs = x <= 0 ? -dx : dx;
+    const double ax = fabs(x);
+    const double u = QPSK_GL_BIG + ax;
+    const double xr = ax - (u - QPSK_GL_BIG);
+    const double xx = xr * xr;
+    const double s = xr + fma(xr * xx, fma(xx, QPSK_GL_SN5, QPSK_GL_SN3), dxs);
+    const double c = fma(xr, dxs, xx * fma(xx, fma(xx, QPSK_GL_CS6, QPSK_GL_CS4), QPSK_GL_CS2));
+    const double *t = tab + qpsk_gl_tab_index_clamped(u);
+    const double sn = t[0], ssn = t[1], cs = t[2], ccs = t[3];
+    double cor = fma(s, ccs, ssn);
+    cor = fma(-c, sn, cor);
+    cor = fma(s, cs, cor);
+    const double r = copysign(sn + cor, x);
+    return ax < 0.126 ? ty : r;
+}
+
+QPSK_GHD static inline double qpsk_gl_do_cos_bf(double x, double dx, const double *tab)
+{
+    const double dxc = x < 0 ? -dx : dx;
+    const double ax = fabs(x);
+    const double u = QPSK_GL_BIG + ax;
+    const double xr = (ax - (u - QPSK_GL_BIG)) + dxc;
+    const double xx = xr * xr;
+    const double s = fma(xr * xx, fma(xx, QPSK_GL_SN5, QPSK_GL_SN3), xr);
+    const double c = xx * fma(xx, fma(xx, QPSK_GL_CS6, QPSK_GL_CS4), QPSK_GL_CS2);
+    const double *t = tab + qpsk_gl_tab_index_clamped(u);
+    const double sn = t[0], ssn = t[1], cs = t[2], ccs = t[3];
+    double cor = fma(-s, ssn, ccs);
+    cor = fma(-c, cs, cor);
+    cor = fma(-s, sn, cor);
+    return cs + cor;
+}
+
+/* full = 0: the caller guarantees |x| < 0x1.921fbp+26 (= 105414348, hi word
+ * 0x419921fb) or a non-finite x, so __branred is left out (the GPU Costas loop
+ * tracks max |theta| and redoes a round with full = 1 if it was exceeded) */
+QPSK_GHD static inline void qpsk_glibc_sincos_bf_k(double x, const double *tab, double *s_out, double *c_out,
+                                                   int full)
+{
+    const uint32_t k = (uint32_t)(qpsk_gl_bits(x) >> 32) & 0x7fffffffu;
+    double aC, daC;
+    int n = qpsk_gl_reduce_sincos(x, &aC, &daC);
+    if (full && k >= 0x419921fbu && k < 0x7ff00000u) n = qpsk_gl_branred(x, &aC, &daC);
+    const double y = QPSK_GL_HP0 - fabs(x);
+    const double aB = y + QPSK_GL_HP1;
+    const double daB = (y - aB) + QPSK_GL_HP1;
+    const int rA = k < 0x3feb6000u;
+    const int rB = k < 0x400368fdu;
+    const double xs = rA ? x : (rB ? aB : aC);
+    const double dxs = rA ? 0.0 : (rB ? daB : daC);
+    const double xc = rA ? x : (rB ? y : aC);
+    const double dxc = rA ? 0.0 : (rB ? QPSK_GL_HP1 : daC);
+    const double DS = qpsk_gl_do_sin_bf(xs, dxs, tab);
+    const double DC = qpsk_gl_do_cos_bf(xc, dxc, tab);
+    const int odd = (n & 1) != 0;
+    double sC = odd ? DC : DS, cC = odd ? DS : DC;
+    sC = (n & 2) ? -sC : sC;
+    cC = ((n + 1) & 2) ? -cC : cC;
+    double s = rA ? DS : (rB ? copysign(DC, x) : sC);
+    double c = rA ? DC : (rB ? DS : cC);
+    if (k < 0x3e500000u) s = x;
+    if (k < 0x3e400000u) c = 1.0;
+    if (k >= 0x7ff00000u) s = c = x - x;   /* glibc: x / x, NaN */
+    *s_out = s;
+    *c_out = c;
+}
+
+#define QPSK_GLIBC_SMALL_LIMIT 0x1.921fbp+26   /* |x| below: qpsk_glibc_sincos_bf_k(full = 0) is exact */
+
+QPSK_GHD static inline void qpsk_glibc_sincos_bf(double x, const double *tab, double *s_out, double *c_out)
+{
+    qpsk_glibc_sincos_bf_k(x, tab, s_out, c_out, 1);
+}
+
+#endif /* QPSK_GLIBC_TRIG_H */

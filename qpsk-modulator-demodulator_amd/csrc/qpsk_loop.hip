@@ -34,6 +34,7 @@
 #include <cstdint>
 #include <type_traits>
 
+#include "qpsk_glibc_trig.h"
 #include "qpsk_kernels.h"
 #include "qpsk_sincos.h"
 
@@ -139,11 +140,13 @@ __global__ void carry_prefix_kernel(LoopArgs a) {
 template <int CAP>
 struct RowStride { static constexpr int value = CAP + 1; };
 
-template <int SPW, int CAP, int KB>
+// TRIG 0: the portable sincos table (qpsk_sincos.h), heads and tails; TRIG 1:
+// glibc's __sincostab (qpsk_glibc_trig.h, 440 doubles), no tails
+template <int SPW, int CAP, int KB, int TRIG>
 struct LoopLds {
     static constexpr int RS = RowStride<CAP>::value;
-    double tab[1024];              // sincos table head (qpsk_sincos.h), at LDS offset 0 so
-    double tab_lo[1024];           // the table index is the whole address; tail (floats, widened)
+    double tab[TRIG ? 440 : 1024];  // sincos table head, at LDS offset 0 so
+    double tab_lo[TRIG ? 2 : 1024]; // the table index is the whole address; tail (floats, widened)
     f2 mf[SPW * Ring<KB>::row];    // sample ring   [stream][mirror | 4 rounds x KB]
     sym_t sym[2 * SPW * RS];       // M&M -> Costas [slot][stream][RS] (see sym_t)
     f2 rot[2 * SPW * RS];          // Costas -> decode
@@ -151,12 +154,12 @@ struct LoopLds {
                                    // cnt[4*SPW + (r & 3)] = their minimum over the batch
 };
 
-template <int MODE, bool DIFF, bool SYMS, int SPW, int CAP, int KB>
+template <int MODE, bool DIFF, bool SYMS, int SPW, int CAP, int KB, int TRIG>
 __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     constexpr int kRing = Ring<KB>::len, kRowS = Ring<KB>::row;
     // one LDS object only: a second __shared__ object would make hipcc drain the
     // loader's LDS-DMA before touching it (cdna_hip_programming.md §5)
-    __shared__ LoopLds<SPW, CAP, KB> L;
+    __shared__ LoopLds<SPW, CAP, KB, TRIG> L;
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -198,9 +201,13 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     const int NR = (wave_max_i32(cnt) + KB - 1) / KB;
     const bool mine = valid && cnt > 0;
 
-    for (int i = threadIdx.x; i < 1024; i += 256) {
-        L.tab[i] = qpsk_sincos_table_dev[i];
-        L.tab_lo[i] = qpsk_sincos_table_dev_lo[i];
+    if constexpr (TRIG) {
+        for (int i = threadIdx.x; i < 440; i += 256) L.tab[i] = qpsk_gl_sincostab_dev[i];
+    } else {
+        for (int i = threadIdx.x; i < 1024; i += 256) {
+            L.tab[i] = qpsk_sincos_table_dev[i];
+            L.tab_lo[i] = qpsk_sincos_table_dev_lo[i];
+        }
     }
     __syncthreads();
 
@@ -666,7 +673,9 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             auto step = [&](int k, auto huge) {
                 const d2 yn = widen(in[k + 1]);   // next symbol, read and widened under this one's chain
                 double sn, cs;
-                if constexpr (decltype(huge)::value) qpsk_sincos_tab(theta, L.tab, L.tab_lo, &sn, &cs);
+                // Math.Sin/Cos = glibc; the fast pass leaves its Payne-Hanek reduction out
+                if constexpr (TRIG) qpsk_glibc_sincos_bf_k(theta, L.tab, &sn, &cs, decltype(huge)::value);
+                else if constexpr (decltype(huge)::value) qpsk_sincos_tab(theta, L.tab, L.tab_lo, &sn, &cs);
                 else qpsk_sincos_tab_core_k(theta, L.tab, L.tab_lo, &K, &sn, &cs);
                 const double mi = y.x * cs + y.y * sn;
                 const double mq = y.y * cs - y.x * sn;
@@ -724,7 +733,10 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 amax = fmax(amax, fabs(theta));
             }
             // fmax drops NaN, which the fast path handles exactly like the full one
-            if (__builtin_expect(__ballot(mine && amax > 0x1p40) != 0, 0)) {
+            // the fast pass's range: |theta| <= 2^40 (portable table), < 105414348
+            // (glibc without __branred)
+            const bool out_of_range = TRIG ? !(amax < QPSK_GLIBC_SMALL_LIMIT) && amax == amax : amax > 0x1p40;
+            if (__builtin_expect(__ballot(mine && out_of_range) != 0, 0)) {
                 theta = theta0;
                 freq = freq0;
                 y = widen(in[0]);
@@ -835,22 +847,28 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     if (a.n_bits) a.n_bits[s] = MODE == kModeDemodulate ? nbits : 0;
 }
 
-template <int SPW, int CAP, int KB>
-static int launch_loop_spw(const LoopArgs &a, const LoopParams &P, int mode, hipStream_t stream) {
+template <int SPW, int CAP, int KB, int TRIG>
+static int launch_loop_spw_t(const LoopArgs &a, const LoopParams &P, int mode, hipStream_t stream) {
     dim3 grid((a.S + SPW - 1) / SPW), block(256);
     const bool syms = a.syms != nullptr;
     const bool diff = P.differential != 0;
     if (mode == kModeConstellation)
-        hipLaunchKernelGGL((loop_kernel<kModeConstellation, false, true, SPW, CAP, KB>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeConstellation, false, true, SPW, CAP, KB, TRIG>), grid, block, 0, stream, a, P);
     else if (diff && syms)
-        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, true, SPW, CAP, KB>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, true, SPW, CAP, KB, TRIG>), grid, block, 0, stream, a, P);
     else if (diff)
-        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, false, SPW, CAP, KB>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, false, SPW, CAP, KB, TRIG>), grid, block, 0, stream, a, P);
     else if (syms)
-        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, true, SPW, CAP, KB>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, true, SPW, CAP, KB, TRIG>), grid, block, 0, stream, a, P);
     else
-        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, false, SPW, CAP, KB>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, false, SPW, CAP, KB, TRIG>), grid, block, 0, stream, a, P);
     return static_cast<int>(grid.x);
+}
+
+template <int SPW, int CAP, int KB>
+static int launch_loop_spw(const LoopArgs &a, const LoopParams &P, int mode, hipStream_t stream) {
+    return P.costas_trig ? launch_loop_spw_t<SPW, CAP, KB, 1>(a, P, mode, stream)
+                         : launch_loop_spw_t<SPW, CAP, KB, 0>(a, P, mode, stream);
 }
 
 int launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant, hipStream_t stream) {

@@ -496,6 +496,11 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
     h->lp.c_alpha = h->d.costas_alpha;
     h->lp.c_beta = h->d.costas_beta;
     h->lp.differential = p->differential ? 1 : 0;
+    if (p->costas_trig != 0 && p->costas_trig != 1) {
+        delete h;
+        return fail(QPSK_ERR_ARGUMENT, "costas_trig must be 0 (portable) or 1 (glibc)");
+    }
+    h->lp.costas_trig = p->costas_trig;
     h->loop_variant = p->loop_variant;
     h->fp.beta = h->d.fll_beta;
     h->fp.alpha = h->d.fll_alpha;

@@ -45,6 +45,7 @@ struct LoopParams {
     double sps, kp, ki;            // MuellerMuller
     double c_alpha, c_beta;        // CostasLoopQpsk
     int32_t differential;
+    int32_t costas_trig;           // 0 portable table sincos, 1 glibc sin/cos (qpsk_glibc_trig.h)
 };
 
 struct FllParams {

@@ -40,10 +40,9 @@ MEM_HOST = 0
 MEM_DEVICE = 1
 MODE_DEMODULATE = 0
 MODE_CONSTELLATION = 1
-# the Costas loop's double sin/cos (CostasLoopQpsk.cs:69-70) on the GPU is
-# glibc's own sin/cos (bit-identical symbols vs the libm oracle) when True,
-# the portable table sincos (within 1 ulp of glibc) when False
-COSTAS_TRIG_EXACT = False
+# qpsk_demod_params.costas_trig: the Costas NCO's Math.Sin/Cos (CostasLoopQpsk.cs:69-70)
+COSTAS_TRIG_PORTABLE = 0      # table sincos, within 1 ulp of glibc (default, faster)
+COSTAS_TRIG_GLIBC = 1         # glibc's own sin/cos: symbols bit-identical to the libm oracle
 
 _i64p = C.POINTER(C.c_int64)
 _u8p = C.POINTER(C.c_uint8)
@@ -67,7 +66,8 @@ class DemodParams(C.Structure):
         ("max_samples_per_call", C.c_int64),
         ("loop_variant", C.c_int32),
         ("iq_balance", C.c_int32),
-        ("reserved", C.c_int32 * 6),
+        ("costas_trig", C.c_int32),
+        ("reserved", C.c_int32 * 5),
     ]
 
 
@@ -243,7 +243,10 @@ def _check(rc):
 def params(sample_rate, symbol_rate, rrc_alpha=0.9, rrc_span=6, symbol_sync_bandwidth=0.0001,
            costas_loop_bandwidth=120.0, cfo_loop_bandwidth=None, differential=True,
            enable_fll=False, vector_lanes=8, device=0, max_samples_per_call=1 << 20,
-           loop_variant=0, iq_balance=False):
+           loop_variant=0, iq_balance=False, costas_trig=0):
+    """qpsk_demod_params (include/qpsk_demod.h); costas_trig = 1 runs the
+    Costas NCO with glibc's own sin / cos (bit-identical symbols vs the
+    libm oracle), 0 the faster portable table sincos."""
     p = DemodParams()
     lib().qpsk_demod_params_init(C.byref(p), int(sample_rate), int(symbol_rate))
     p.rrc_alpha = float(np.float32(rrc_alpha))
@@ -259,6 +262,7 @@ def params(sample_rate, symbol_rate, rrc_alpha=0.9, rrc_span=6, symbol_sync_band
     p.max_samples_per_call = int(max_samples_per_call)
     p.loop_variant = int(loop_variant)
     p.iq_balance = 1 if iq_balance else 0
+    p.costas_trig = int(costas_trig)
     return p
 
 

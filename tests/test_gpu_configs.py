@@ -14,8 +14,9 @@ the real glibc trig (what .NET's Math.Sin/Cos and MathF.Sin/Cos reach on
 Linux), one oracle demodulator per stream fed the same seven calls.
 
 Bar: bits identical on every call; rotated symbols of the first (fresh
-state) and the seventh (steady state) call identical, or within SYM_TOL where
-the GPU's Costas sincos is not glibc's (qpsk_amd.COSTAS_TRIG_EXACT).
+state) and the seventh (steady state) call bit-identical with the Costas NCO
+on glibc's own sin/cos (costas_trig = 1), within SYM_TOL with the default
+portable table sincos (costas_trig = 0, within 1 ulp of glibc).
 """
 from concurrent.futures import ThreadPoolExecutor
 
@@ -62,8 +63,8 @@ def _oracle_stream(row, sps, span, fll):
     return [d.demodulate_ex(row) for _ in range(CALLS)]
 
 
-@pytest.mark.parametrize("key", list(CASES))
-def test_baseline_workload_seven_calls_vs_libm_oracle(key):
+@pytest.mark.parametrize("key,trig", [(k, 0) for k in CASES] + [("c3", 1), ("c5", 1)])
+def test_baseline_workload_seven_calls_vs_libm_oracle(key, trig):
     import torch
     c = CASES[key]
     S, sps, span, imp = c["S"], c["sps"], c["span"], c["impaired"]
@@ -74,7 +75,7 @@ def test_baseline_workload_seven_calls_vs_libm_oracle(key):
     del _tx
     assert iq.stride(0) * 4 * (S - 1) > (16 << 30)   # last rows 32-64 GiB in
     b = Q.BatchDemodulator(S, Q.params(K.FS, K.FS // sps, K.ALPHA, span, enable_fll=imp,
-                                       max_samples_per_call=N))
+                                       max_samples_per_call=N, costas_trig=trig))
     ms = b.max_symbols(N)
     stream = torch.cuda.Stream(dev)
     b.set_stream(stream.cuda_stream)
@@ -112,7 +113,7 @@ def test_baseline_workload_seven_calls_vs_libm_oracle(key):
 
     with ThreadPoolExecutor(max_workers=len(idx)) as ex:
         ref = list(ex.map(lambda r: _oracle_stream(r, sps, span, imp), list(host)))
-    exact = Q.COSTAS_TRIG_EXACT
+    exact = trig == 1
     for j, s in enumerate(idx):
         for k in range(CALLS):
             gb, gnb, gsy, gns = (x[j] if x is not None else None for x in got[k])
