@@ -129,9 +129,10 @@ def free_port():
 # parity of the timed handle against the CPU oracle
 # ---------------------------------------------------------------------------
 def compare_rows(gpu_bits, gpu_nb, ref_bits, ref_nb, gpu_syms=None, gpu_ns=None, ref_syms=None,
-                 ref_ns=None):
+                 ref_ns=None, sym_exact=False):
     """Per-stream comparison of packed bit rows (+ symbols when both sides
-    have them).  Returns (mismatching stream indices, max |symbol error|)."""
+    have them; sym_exact: a symbol that is not bit-identical fails the stream).
+    Returns (mismatching stream indices, max |symbol error|)."""
     import numpy as np
     bad = []
     max_err = 0.0
@@ -150,6 +151,8 @@ def compare_rows(gpu_bits, gpu_nb, ref_bits, ref_nb, gpu_syms=None, gpu_ns=None,
             if ok and ns:
                 d = np.abs(gpu_syms[i, : 2 * ns].astype(np.float64) - ref_syms[i, : 2 * ns])
                 max_err = max(max_err, float(np.nanmax(d)) if d.size else 0.0)
+                if sym_exact:
+                    ok = np.array_equal(gpu_syms[i, : 2 * ns].view(np.uint32), ref_syms[i, : 2 * ns].view(np.uint32))
         if not ok:
             bad.append(i)
     return bad, max_err
@@ -181,7 +184,7 @@ def pick_streams(S, n_cover, tail=64):
 
 
 def cpu_leg(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, n, budget_s, threads, single_streams=8,
-            n_cover=None):
+            n_cover=None, costas_trig=0):
     """CPU baseline + parity at scale: the oracle (glibc trig) on the host
     cores over a time-bounded subset of the timed batch, timed, and its bit
     rows / symbols compared with the GPU's rows of the same streams.
@@ -215,7 +218,7 @@ def cpu_leg(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, n, budget_s, thre
     gnb = rows_to_host(nbits_dev, idx)
     gsy = rows_to_host(syms_dev, idx) if want_syms else None
     gns = rows_to_host(nsyms_dev, idx) if want_syms else None
-    bad, max_err = compare_rows(gb, gnb, rb, rnb, gsy, gns, rsy, rns)
+    bad, max_err = compare_rows(gb, gnb, rb, rnb, gsy, gns, rsy, rns, sym_exact=bool(costas_trig))
     rate = len(idx) * n / dt / 1e6
     cpu = {"value": round(rate, 2), "unit": "MSa/s", "cores": threads, "kind": "port",
            "single_core": round(ns1 * n / dt1 / 1e6, 2), "cpu_model": cpu_model(),
@@ -235,23 +238,25 @@ def cpu_leg(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, n, budget_s, thre
               "streams": len(idx), "first_stream": idx[0], "last_stream": idx[-1],
               "mismatching_streams": len(bad), "mismatch_examples": bad[:8],
               "max_sym_err": (round(max_err, 9) if want_syms else None),
-              "sym_tol": 1e-5 if not cfg["fll"] else 1e-4,
+              "sym_tol": 0.0 if costas_trig else (1e-5 if not cfg["fll"] else 1e-4),
               "max_row_offset_GiB": round(idx[-1] * iq.stride(0) * 4 / 2**30, 2)}
     if not want_syms:
         parity["note"] = "bits only: no HBM left for a symbol copy of the whole batch"
     return cpu, parity
 
 
-def portable_check(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, idx):
+def portable_check(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, idx, costas_trig=0):
     """Bit-exact check (bits AND symbols) of a few streams of the timed handle
-    against the portable-trig oracle, which shares the GPU's sincos."""
+    against the oracle with the GPU's own Costas trig: the portable table
+    sincos (costas_trig 0) or glibc's sin/cos (costas_trig 1, the libm oracle)."""
     import numpy as np
     import torch
     import oracle as O
     host = rows_to_host(iq, idx)
     rb, rnb, rsy, rns = O.demod_batch_packed(host, FS, FS // cfg["sps"], n_threads=len(idx),
                                              want_syms=syms_dev is not None, rrc_alpha=ALPHA,
-                                             rrc_span=cfg["span"], trig=O.TRIG_PORTABLE,
+                                             rrc_span=cfg["span"],
+                                             trig=O.TRIG_LIBM if costas_trig else O.TRIG_PORTABLE,
                                              enable_fll=cfg["fll"])
     gb = rows_to_host(bits_dev, idx)
     gnb = rows_to_host(nbits_dev, idx)
@@ -604,7 +609,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
         errs, total_bits, lost, slips = ber_after_lock(bits, nbits, tx, min(S, 32))
         if not args.no_parity:
             idx = [0, 1, S - 2, S - 1] if S >= 4 else list(range(S))
-            bad_bits, bad_syms = portable_check(iq, bits, nbits, syms, nsyms, cfg, idx)
+            bad_bits, bad_syms = portable_check(iq, bits, nbits, syms, nsyms, cfg, idx, args.costas_trig)
             n_port = len(idx)
             if not args.no_cpu_baseline:
                 # every rank: the libm oracle on its own shard (N = 1: as many
@@ -612,7 +617,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
                 # 64 of the shard, on this rank's share of the host threads)
                 threads = args.cpu_threads or max(1, (os.cpu_count() or 1) // world)
                 cpu, par = cpu_leg(iq, bits, nbits, syms, nsyms, cfg, n, args.cpu_seconds, threads,
-                                   n_cover=None if world == 1 else min(S, 72))
+                                   n_cover=None if world == 1 else min(S, 72), costas_trig=args.costas_trig)
                 libm_bad, libm_streams = par["mismatching_streams"], par["streams"]
                 if rank == 0:
                     rec["cpu_baseline"], rec["parity_vs_libm_oracle"] = cpu, par
@@ -671,8 +676,9 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
         "parity_vs_portable_oracle": (
             "not checked" if (args.no_parity or args.timed_only) else
             {"streams": n_port, "bit_mismatch_streams": bad_bits, "symbol_mismatch_streams": bad_syms,
+             "oracle": "glibc trig (libm)" if args.costas_trig else "portable trig",
              "note": "first and last two streams of every rank's shard; bits and symbols must be "
-                     "bit-identical (the oracle shares the GPU's sincos)"}),
+                     "bit-identical (the oracle runs the GPU's own Costas trig)"}),
         **rec,
     }
     if rec.get("cpu_baseline") is None:

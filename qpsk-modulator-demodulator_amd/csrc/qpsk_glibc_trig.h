@@ -368,6 +368,99 @@ QPSK_GHD static inline void qpsk_glibc_sincos_bf_k(double x, const double *tab, 
 
 #define QPSK_GLIBC_SMALL_LIMIT 0x1.921fbp+26   /* |x| below: qpsk_glibc_sincos_bf_k(full = 0) is exact */
 
+/* ---- split form: two lanes per argument ------------------------------------
+ * The do_sin and the do_cos of the branch-free form run on two lanes of the
+ * same wave (the GPU Costas loop: lane l and lane l + 32 carry the same
+ * stream), each with its own layout of the table so that one code path
+ * serves both:
+ *   h = 0 (do_sin):  {ccs, ssn, sn, cs}     cor = ((s*T0 + T1) - c*T2) + s*T3
+ *   h = 1 (do_cos):  {-ssn, ccs, cs, -sn}   r = T2 + cor
+ * (s*(-ssn) + ccs rounds as ccs - s*ssn, an fma with a negated operand is
+ * the same rounding), and the sin-only terms fold in as +0 / x*0 where the
+ * cos has none (exact: those terms add +0 to a value that is never -0).
+ * Every step equals qpsk_gl_do_sin_bf (h = 0) / qpsk_gl_do_cos_bf (h = 1);
+ * tools/check_glibc_sin.c -DWITH_PRODUCT checks the assembled pair. */
+QPSK_GHD static inline void qpsk_gl_half_tables(const double *tab, int i, double *ts4, double *tc4)
+{
+    /* entry i of the two layouts from __sincostab entry i = {sn, ssn, cs, ccs} */
+    const double sn = tab[4 * i], ssn = tab[4 * i + 1], cs = tab[4 * i + 2], ccs = tab[4 * i + 3];
+    ts4[0] = ccs; ts4[1] = ssn; ts4[2] = sn; ts4[3] = cs;
+    tc4[0] = -ssn; tc4[1] = ccs; tc4[2] = cs; tc4[3] = -sn;
+}
+
+QPSK_GHD static inline double qpsk_gl_do_half(double x, double dx, int h, const double *tabh)
+{
+    const double ty = qpsk_gl_taylor_sin(x, dx);
+    const int flip = h ? (x < 0) : (x <= 0);
+    const double d = flip ? -dx : dx;
+    const double ax = fabs(x);
+    const double u = QPSK_GL_BIG + ax;
+    const double xr = (ax - (u - QPSK_GL_BIG)) + (h ? d : 0.0);
+    const double xx = xr * xr;
+    const double q = xr * xx;
+    const double p = fma(xx, QPSK_GL_SN5, QPSK_GL_SN3);
+    const double s = (h ? 0.0 : xr) + fma(q, p, h ? xr : d);
+    const double c = fma(xr, h ? 0.0 : d, xx * fma(xx, fma(xx, QPSK_GL_CS6, QPSK_GL_CS4), QPSK_GL_CS2));
+    const double *t = tabh + qpsk_gl_tab_index_clamped(u);
+    double cor = fma(s, t[0], t[1]);
+    cor = fma(-c, t[2], cor);
+    cor = fma(s, t[3], cor);
+    const double r = t[2] + cor;
+    return h ? r : (ax < 0.126 ? ty : copysign(r, x));
+}
+
+/* the argument of half h (0: do_sin, 1: do_cos) and the region bookkeeping */
+typedef struct {
+    double xa, dxa;
+    int n, rA, rB;
+} qpsk_gl_split_arg;
+
+QPSK_GHD static inline qpsk_gl_split_arg qpsk_gl_split_prepare(double x, int h, int full)
+{
+    qpsk_gl_split_arg g;
+    const uint32_t k = (uint32_t)(qpsk_gl_bits(x) >> 32) & 0x7fffffffu;
+    double aC, daC;
+    g.n = qpsk_gl_reduce_sincos(x, &aC, &daC);
+    if (full && k >= 0x419921fbu && k < 0x7ff00000u) g.n = qpsk_gl_branred(x, &aC, &daC);
+    const double y = QPSK_GL_HP0 - fabs(x);
+    const double aB = y + QPSK_GL_HP1;
+    const double daB = (y - aB) + QPSK_GL_HP1;
+    g.rA = k < 0x3feb6000u;
+    g.rB = k < 0x400368fdu;
+    g.xa = g.rA ? x : (g.rB ? (h ? y : aB) : aC);
+    g.dxa = g.rA ? 0.0 : (g.rB ? (h ? QPSK_GL_HP1 : daB) : daC);
+    return g;
+}
+
+/* sin and cos from DS = do_sin and DC = do_cos of the prepared arguments */
+QPSK_GHD static inline void qpsk_gl_split_finish(double x, const qpsk_gl_split_arg *g, double DS, double DC,
+                                                 double *s_out, double *c_out)
+{
+    const uint32_t k = (uint32_t)(qpsk_gl_bits(x) >> 32) & 0x7fffffffu;
+    /* region A: (DS, DC); B: (+-DC, DS); C: by the parity of n, signs by bits
+     * of n and n + 1.  swap and both signs as integer logic, then two selects */
+    const int swap = g->rA ? 0 : (g->rB ? 1 : (g->n & 1));
+    double s = swap ? DC : DS, c = swap ? DS : DC;
+    const uint64_t sgn = 0x8000000000000000ull;
+    const uint64_t ns = g->rA ? 0 : (g->rB ? (qpsk_gl_bits(x) & sgn) : ((g->n & 2) ? sgn : 0));
+    const uint64_t nc = (g->rA || g->rB) ? 0 : (((g->n + 1) & 2) ? sgn : 0);
+    s = qpsk_gl_from_bits(qpsk_gl_bits(s) ^ ns);
+    c = qpsk_gl_from_bits(qpsk_gl_bits(c) ^ nc);
+    if (k < 0x3e500000u) s = x;
+    *s_out = s;
+    *c_out = c;
+}
+
+/* host form of the split evaluation (both halves in one thread), for the checker */
+QPSK_GHD static inline void qpsk_glibc_sincos_split_host(double x, const double *tabs, const double *tabc,
+                                                         double *s_out, double *c_out)
+{
+    const qpsk_gl_split_arg g0 = qpsk_gl_split_prepare(x, 0, 1), g1 = qpsk_gl_split_prepare(x, 1, 1);
+    const double DS = qpsk_gl_do_half(g0.xa, g0.dxa, 0, tabs);
+    const double DC = qpsk_gl_do_half(g1.xa, g1.dxa, 1, tabc);
+    qpsk_gl_split_finish(x, &g0, DS, DC, s_out, c_out);
+}
+
 QPSK_GHD static inline void qpsk_glibc_sincos_bf(double x, const double *tab, double *s_out, double *c_out)
 {
     qpsk_glibc_sincos_bf_k(x, tab, s_out, c_out, 1);

@@ -118,6 +118,18 @@ __device__ __forceinline__ int wave_max_i32(int v) {
     return __builtin_amdgcn_readfirstlane(v);
 }
 
+// r of the lower half (lanes 0-31) and of the upper half (lanes 32-63) of the
+// wave, each into every lane: v_permlane32_swap exchanges the upper half of
+// its first operand with the lower half of its second (lo and hi dwords)
+__device__ __forceinline__ void swap_halves(double r, double *lower, double *upper) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, r);
+    const uint32_t lo = static_cast<uint32_t>(b), hi = static_cast<uint32_t>(b >> 32);
+    const auto pl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto ph = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    *lower = __builtin_bit_cast(double, (static_cast<uint64_t>(ph[0]) << 32) | pl[0]);
+    *upper = __builtin_bit_cast(double, (static_cast<uint64_t>(ph[1]) << 32) | pl[1]);
+}
+
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
     const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), l);
     const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32), l);
@@ -141,11 +153,12 @@ template <int CAP>
 struct RowStride { static constexpr int value = CAP + 1; };
 
 // TRIG 0: the portable sincos table (qpsk_sincos.h), heads and tails; TRIG 1:
-// glibc's __sincostab (qpsk_glibc_trig.h, 440 doubles), no tails
+// glibc's __sincostab in the split form's two layouts (qpsk_glibc_trig.h:
+// do_sin rows at 0, do_cos rows at 440), no tails
 template <int SPW, int CAP, int KB, int TRIG>
 struct LoopLds {
     static constexpr int RS = RowStride<CAP>::value;
-    double tab[TRIG ? 440 : 1024];  // sincos table head, at LDS offset 0 so
+    double tab[TRIG ? 880 : 1024];  // sincos table head, at LDS offset 0 so
     double tab_lo[TRIG ? 2 : 1024]; // the table index is the whole address; tail (floats, widened)
     f2 mf[SPW * Ring<KB>::row];    // sample ring   [stream][mirror | 4 rounds x KB]
     sym_t sym[2 * SPW * RS];       // M&M -> Costas [slot][stream][RS] (see sym_t)
@@ -202,7 +215,8 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     const bool mine = valid && cnt > 0;
 
     if constexpr (TRIG) {
-        for (int i = threadIdx.x; i < 440; i += 256) L.tab[i] = qpsk_gl_sincostab_dev[i];
+        for (int i = threadIdx.x; i < 110; i += 256)
+            qpsk_gl_half_tables(qpsk_gl_sincostab_dev, i, L.tab + 4 * i, L.tab + 440 + 4 * i);
     } else {
         for (int i = threadIdx.x; i < 1024; i += 256) {
             L.tab[i] = qpsk_sincos_table_dev[i];
@@ -630,10 +644,19 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
 #endif
     if (wave == 2) {
         // ============================================================ Costas
+        // TRIG 1: lanes l and l + 32 both run stream l (SPW <= 32), for the split
+        // glibc sincos: the lower lane evaluates the do_sin, the upper the do_cos
+        // (qpsk_glibc_trig.h), and v_permlane32_swap hands each its partner's
+        // result; both halves then run the same Costas update
+        const int cl = TRIG ? (lane & 31) : lane;
+        const bool cmine = TRIG ? (__shfl(mine ? 1 : 0, cl, 64) != 0) : mine;
+        const int csc = TRIG ? __shfl(sc, cl, 64) : sc;
+        const int half = TRIG ? (lane >> 5) : 0;
+        const double *tabh = L.tab + (half ? 440 : 0);
         double theta = 0.0, freq = 0.0;
-        if (mine) {
-            theta = a.state[sc].theta;
-            freq = a.state[sc].freq;
+        if (cmine) {
+            theta = a.state[csc].theta;
+            freq = a.state[csc].freq;
         }
         double ca = P.c_alpha, cb = P.c_beta;
         double kTwoPi = 2.0 * 3.14159265358979311600;
@@ -656,10 +679,11 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             STAMP(tl);
             const int slot = (r - 1) & 1;
             const int mlo = __builtin_amdgcn_readfirstlane(L.cnt[4 * SPW + ((r - 1) & 3)]);
-            if (lane >= SPW) continue;   // exec = the batch's lanes for the whole round
-            const int m = mine ? L.cnt[((r - 1) & 3) * SPW + lane] : 0;
-            const sym_t *in = L.sym + (slot * SPW + lane) * L.RS;
-            f2 *out = L.rot + (slot * SPW + lane) * L.RS;
+            if (cl >= SPW) continue;   // exec = the batch's lanes for the whole round
+            const int m = cmine ? L.cnt[((r - 1) & 3) * SPW + cl] : 0;
+            const sym_t *in = L.sym + (slot * SPW + cl) * L.RS;
+            // (TRIG 1: both lanes of a stream store the same value to the same slot)
+            f2 *out = L.rot + (slot * SPW + cl) * L.RS;
             d2 y;
             // CostasLoopQpsk.cs:63-92: double NCO, float I/O (y widened to double).
             // HUGE: theta may exceed the table reduction's range (|theta| <= 2^40,
@@ -674,7 +698,13 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const d2 yn = widen(in[k + 1]);   // next symbol, read and widened under this one's chain
                 double sn, cs;
                 // Math.Sin/Cos = glibc; the fast pass leaves its Payne-Hanek reduction out
-                if constexpr (TRIG) qpsk_glibc_sincos_bf_k(theta, L.tab, &sn, &cs, decltype(huge)::value);
+                if constexpr (TRIG) {
+                    const qpsk_gl_split_arg g = qpsk_gl_split_prepare(theta, half, decltype(huge)::value);
+                    const double rh = qpsk_gl_do_half(g.xa, g.dxa, half, tabh);
+                    double DS, DC;
+                    swap_halves(rh, &DS, &DC);
+                    qpsk_gl_split_finish(theta, &g, DS, DC, &sn, &cs);
+                }
                 else if constexpr (decltype(huge)::value) qpsk_sincos_tab(theta, L.tab, L.tab_lo, &sn, &cs);
                 else qpsk_sincos_tab_core_k(theta, L.tab, L.tab_lo, &K, &sn, &cs);
                 const double mi = y.x * cs + y.y * sn;
@@ -736,7 +766,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             // the fast pass's range: |theta| <= 2^40 (portable table), < 105414348
             // (glibc without __branred)
             const bool out_of_range = TRIG ? !(amax < QPSK_GLIBC_SMALL_LIMIT) && amax == amax : amax > 0x1p40;
-            if (__builtin_expect(__ballot(mine && out_of_range) != 0, 0)) {
+            if (__builtin_expect(__ballot(cmine && out_of_range) != 0, 0)) {
                 theta = theta0;
                 freq = freq0;
                 y = widen(in[0]);

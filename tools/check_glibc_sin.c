@@ -35,6 +35,9 @@ static uint64_t next64(void)
 static double uni(double lo, double hi) { return lo + (hi - lo) * ((next64() >> 11) * 0x1p-53); }
 
 static long n_checked, n_bad;
+#ifdef WITH_PRODUCT
+static double g_tabs[440], g_tabc[440];   /* the split form's two table layouts */
+#endif
 static double (*volatile libm_sin)(double) = sin;
 static double (*volatile libm_cos)(double) = cos;
 
@@ -55,10 +58,16 @@ static void check(double x)
         if (n_bad < 20) printf("x=%a product sin %a cos %a vs oracle %a %a\n", x, ps, pc, s, c);
         ++n_bad;
     }
-    double bs, bc;   /* the branch-free form the GPU Costas loop runs */
+    double bs, bc;   /* the branch-free form */
     qpsk_glibc_sincos_bf(x, qpsk_gl_sincostab_host, &bs, &bc);
     if (!same(bs, s) || !same(bc, c)) {
         if (n_bad < 20) printf("x=%a branch-free sin %a cos %a vs oracle %a %a\n", x, bs, bc, s, c);
+        ++n_bad;
+    }
+    double ss, sc;   /* the split form the GPU Costas loop runs (two lanes per argument) */
+    qpsk_glibc_sincos_split_host(x, g_tabs, g_tabc, &ss, &sc);
+    if (!same(ss, s) || !same(sc, c)) {
+        if (n_bad < 20) printf("x=%a split sin %a cos %a vs oracle %a %a\n", x, ss, sc, s, c);
         ++n_bad;
     }
 #endif
@@ -88,6 +97,9 @@ static void sweep(double x, int ulps)
 int main(int argc, char **argv)
 {
     const long scale = argc > 1 ? atol(argv[1]) : 1;
+#ifdef WITH_PRODUCT
+    for (int i = 0; i < 110; ++i) qpsk_gl_half_tables(qpsk_gl_sincostab_host, i, g_tabs + 4 * i, g_tabc + 4 * i);
+#endif
     for (long i = 0; i < scale * (1L << 24); ++i) check(uni(-8.0, 8.0));
     printf("[-8, 8]: %ld checked, %ld differ\n", n_checked, n_bad);
     for (long i = 0; i < scale * (1L << 22); ++i) check(uni(-0x1p27, 0x1p27));
