@@ -86,6 +86,34 @@ namespace qpsk {
 int set_last_error(int code, const std::string &msg) { return fail(code, msg); }
 }  // namespace qpsk
 
+namespace {
+struct Call {
+    int32_t mode;
+    const float *iq;
+    int64_t stride_floats;
+    int64_t n_samples;
+    const int64_t *lengths;
+    int32_t mem;
+    uint8_t *bits;
+    int64_t bits_stride_bytes;
+    int64_t *n_bits;
+    float *syms;
+    int64_t syms_stride_floats;
+    int64_t *n_syms;
+    int64_t n_call = 0;    // derived by validate()
+    int64_t max_sym = 0;
+    // internal chunk of a longer call: outputs appended to dst_* at the running
+    // offsets d_acc (first chunk: from 0), totals to n_bits / n_syms after the last
+    bool append = false, first = false, last = false;
+    uint8_t *dst_bits = nullptr;
+    int64_t dst_bits_stride = 0;
+    float *dst_syms = nullptr;
+    int64_t dst_syms_stride = 0;
+    int64_t *dst_n_bits = nullptr;   // device; written after the last chunk
+    int64_t *dst_n_syms = nullptr;
+};
+}  // namespace
+
 struct qpsk_demod {
     qpsk_demod_params p{};
     int S = 0;
@@ -153,6 +181,14 @@ struct qpsk_demod {
     bool gate_pending = false;       // the next FIR has a loop launch to wait for
     int last_back = -1;              // boundary buffer of the newest back stage, -1 = none
     int64_t *h_len[2] = {nullptr, nullptr};   // pinned staging of per-call lengths
+    // FLL on: the back stage (loop kernel) of the newest call is issued by the
+    // next call, after that call's FLL, or by a flush (see process_async_one)
+    hipEvent_t e_fll = nullptr;
+    bool deferred = false;
+    Call dcall{};
+    int dbuf = 0;
+    const int64_t *dlen = nullptr;
+    unsigned long long *dkt = nullptr;
 };
 
 namespace qpsk {
@@ -169,37 +205,18 @@ namespace {
 // The newest pipelined call's back stage, or nullptr.
 hipEvent_t last_async(const qpsk_demod *h) { return h->last_back >= 0 ? h->e_back[h->last_back] : nullptr; }
 
-// Host wait for every pipelined call issued so far.
-int drain_async(const qpsk_demod *h) {
+int flush_deferred(qpsk_demod *h);   // issues a deferred back stage (with the stage runners)
+
+// Host wait for every pipelined call issued so far (a deferred back stage is
+// issued first: every caller of this waits for all of the handle's work).
+int drain_async(const qpsk_demod *hc) {
+    qpsk_demod *h = const_cast<qpsk_demod *>(hc);
+    int rc;
+    if ((rc = flush_deferred(h))) return rc;
     if (hipEvent_t e = last_async(h)) HIP_TRY(hipEventSynchronize(e));
     return QPSK_OK;
 }
 
-struct Call {
-    int32_t mode;
-    const float *iq;
-    int64_t stride_floats;
-    int64_t n_samples;
-    const int64_t *lengths;
-    int32_t mem;
-    uint8_t *bits;
-    int64_t bits_stride_bytes;
-    int64_t *n_bits;
-    float *syms;
-    int64_t syms_stride_floats;
-    int64_t *n_syms;
-    int64_t n_call = 0;    // derived by validate()
-    int64_t max_sym = 0;
-    // internal chunk of a longer call: outputs appended to dst_* at the running
-    // offsets d_acc (first chunk: from 0), totals to n_bits / n_syms after the last
-    bool append = false, first = false, last = false;
-    uint8_t *dst_bits = nullptr;
-    int64_t dst_bits_stride = 0;
-    float *dst_syms = nullptr;
-    int64_t dst_syms_stride = 0;
-    int64_t *dst_n_bits = nullptr;   // device; written after the last chunk
-    int64_t *dst_n_syms = nullptr;
-};
 
 int validate(qpsk_demod *h, Call &c) {
     if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
@@ -396,25 +413,21 @@ int pipe_setup(qpsk_demod *h) {
         HIP_TRY(hipEventCreateWithFlags(&h->e_back[b], hipEventDisableTiming));
         HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h->h_len[b]), h->S * sizeof(int64_t)));
     }
-    if (!h->p.enable_fll) {
-        HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void **>(&h->d_resident), sizeof(unsigned long long),
-                                      hipMallocSignalMemory));
-        HIP_TRY(hipMemset(h->d_resident, 0, sizeof(unsigned long long)));
-    }
+    HIP_TRY(hipEventCreateWithFlags(&h->e_fll, hipEventDisableTiming));
+    HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void **>(&h->d_resident), sizeof(unsigned long long),
+                                  hipMallocSignalMemory));
+    HIP_TRY(hipMemset(h->d_resident, 0, sizeof(unsigned long long)));
     int rc;
     if (!h->d_lengths[1] && (rc = dev_alloc(&h->d_lengths[1], h->S))) return rc;
-    // the second boundary buffer: FLL output rows with the FLL on, MF rows
-    // otherwise.  No room for it (batches near the 288 GB) -> calls still
-    // queue back to back, but each front stage waits for the previous back stage
+    // the second boundary buffer: MF rows (the FIR of one call writes one while
+    // the loop kernel of the previous call reads the other).  No room for it
+    // (batches near the 288 GB) -> calls still queue back to back, but each
+    // front stage waits for the previous back stage
     const size_t S = static_cast<size_t>(h->S);
-    hipError_t e;
-    if (h->p.enable_fll)
-        e = hipMalloc(reinterpret_cast<void **>(&h->d_fll_out[1]), 2 * S * h->n_max * sizeof(float));
-    else
-        e = hipMalloc(reinterpret_cast<void **>(&h->d_mf[1]), 2 * S * h->mf_stride * sizeof(float));
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&h->d_mf[1]), 2 * S * h->mf_stride * sizeof(float));
     if (e == hipSuccess) {
         h->pipe_bufs = 2;
-        if (!h->p.enable_fll) HIP_TRY(hipMemset(h->d_mf[1], 0, 2 * S * h->mf_stride * sizeof(float)));
+        HIP_TRY(hipMemset(h->d_mf[1], 0, 2 * S * h->mf_stride * sizeof(float)));
     } else {
         (void)hipGetLastError();
         h->pipe_bufs = 1;
@@ -623,6 +636,7 @@ int qpsk_demod_destroy(qpsk_demod *h) {
     hipFree(h->d_xbits);
     hipFree(h->d_xsyms);
     if (h->e_in) hipEventDestroy(h->e_in);
+    if (h->e_fll) hipEventDestroy(h->e_fll);
     if (h->s_front) hipStreamDestroy(h->s_front);
     if (h->s_back) hipStreamDestroy(h->s_back);
     if (h->own_stream && h->stream) hipStreamDestroy(h->stream);
@@ -738,6 +752,7 @@ int process_one(qpsk_demod *h, const Call &c) {
     hipStream_t st = h->stream;
     HIP_TRY(hipSetDevice(h->p.device));
     // pipelined calls issued before this one finish first (they share the state)
+    if ((rc = flush_deferred(h))) return rc;
     if (hipEvent_t e = last_async(h)) HIP_TRY(hipStreamWaitEvent(st, e, 0));
     unsigned long long *kt = next_kt(h);
     if (mem == QPSK_MEM_HOST && !c.append) HIP_TRY(hipMemsetAsync(h->d_flags + 1, 0, sizeof(uint32_t), st));
@@ -811,14 +826,44 @@ int process_async_one(qpsk_demod *h, const Call &c) {
     }
     float *mf;
     if (h->p.enable_fll) {
-        // front = FLL into boundary rows b; back = FIR (MF rows 0) + loop
-        if (n_call > 0) run_fll(h, x, x_stride, d_len, n_call, h->d_fll_out[b], F, kt);
-        HIP_TRY(hipEventRecord(h->e_front[b], F));
-        HIP_TRY(hipStreamWaitEvent(B, h->e_front[b], 0));
-        mf = h->d_mf[0];
-        if ((rc = run_fir(h, n_call > 0 ? h->d_fll_out[b] : x, n_call > 0 ? h->n_max : x_stride, d_len,
-                          n_call, mf, B, kt)))
+        // FLL on (C5): the FLL keeps every SIMD's VALU busy with one wave each
+        // (DESIGN.md 3.3), so a kernel beside it gains what it takes from it,
+        // and the launches swing (FIR 48-198, loop 23-218 ms at C5 in round 2).
+        // The FIR and the loop kernel overlap well (the FLL-off pipeline).  So:
+        //   F: FLL(k) alone -> [B: loop(k-1) after FLL(k)] -> F: FIR(k) once
+        //   loop(k-1) holds its CUs (residency gate) -> FIR(k) || loop(k-1)
+        // The loop kernel of call k is issued by call k+1 after its FLL, or by
+        // a flush (pipeline_wait, a synchronous call, state access, destroy).
+        // FLL(k) waited above for loop(k-2), the last reader of MF rows b, and
+        // follows FIR(k-1) on F, so it runs alone.
+        if (n_call > 0) run_fll(h, x, x_stride, d_len, n_call, h->d_fll_out[0], F, kt);
+        HIP_TRY(hipEventRecord(h->e_fll, F));
+        if (h->deferred) {
+            Call dc = h->dcall;
+            HIP_TRY(hipStreamWaitEvent(B, h->e_fll, 0));
+            const int db = h->dbuf;
+            h->deferred = false;
+            if ((rc = run_loop(h, dc, h->dlen, h->d_mf[db], B, h->dkt, h->d_resident))) return rc;
+            HIP_TRY(hipEventRecord(h->e_back[db], B));
+            h->back_rec[db] = true;
+            h->last_back = db;
+        }
+        if (h->gate_pending)
+            HIP_TRY(hipStreamWaitValue64(F, h->d_resident, h->resident_gate, hipStreamWaitValueGte));
+        h->gate_pending = false;
+        mf = h->d_mf[b];
+        if ((rc = run_fir(h, n_call > 0 ? h->d_fll_out[0] : x, n_call > 0 ? h->n_max : x_stride, d_len, n_call,
+                          mf, F, kt)))
             return rc;
+        HIP_TRY(hipEventRecord(h->e_front[b], F));
+        h->front_rec[b] = true;
+        h->dcall = c;
+        h->dbuf = b;
+        h->dlen = d_len;
+        h->dkt = kt;
+        h->deferred = true;
+        // one MF buffer only: nothing can overlap, issue the back stage now
+        return h->pipe_bufs == 2 ? QPSK_OK : flush_deferred(h);
     } else {
         // front = FIR into MF rows b; back = loop.  FIR(k+1) and loop(k) both
         // become ready when a stage of call k-1 or k ends, and whichever is
@@ -843,10 +888,25 @@ int process_async_one(qpsk_demod *h, const Call &c) {
         HIP_TRY(hipStreamWaitEvent(B, h->e_front[b], 0));
     }
     h->front_rec[b] = true;
-    if ((rc = run_loop(h, c, d_len, mf, B, kt, h->p.enable_fll ? nullptr : h->d_resident))) return rc;
+    if ((rc = run_loop(h, c, d_len, mf, B, kt, h->d_resident))) return rc;
     HIP_TRY(hipEventRecord(h->e_back[b], B));
     h->back_rec[b] = true;
     h->last_back = b;
+    return QPSK_OK;
+}
+
+// The deferred back stage (FLL on) after its own FIR only: nothing follows it.
+int flush_deferred(qpsk_demod *h) {
+    if (!h->deferred) return QPSK_OK;
+    HIP_TRY(hipSetDevice(h->p.device));
+    const int db = h->dbuf;
+    h->deferred = false;
+    HIP_TRY(hipStreamWaitEvent(h->s_back, h->e_front[db], 0));
+    int rc;
+    if ((rc = run_loop(h, h->dcall, h->dlen, h->d_mf[db], h->s_back, h->dkt))) return rc;
+    HIP_TRY(hipEventRecord(h->e_back[db], h->s_back));
+    h->back_rec[db] = true;
+    h->last_back = db;
     return QPSK_OK;
 }
 
@@ -1024,6 +1084,8 @@ int qpsk_demod_status(qpsk_demod *h, uint32_t *flags) {
 
 int qpsk_demod_pipeline_wait(qpsk_demod *h, void *hip_stream) {
     if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
+    int rc;
+    if ((rc = flush_deferred(h))) return rc;
     hipEvent_t e = last_async(h);
     if (!e) return QPSK_OK;
     if (hip_stream) HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(hip_stream), e, 0));

@@ -154,6 +154,13 @@ def test_gpu_tad_sps8(Q):
     assert np.array_equal(syms[0, : 2 * int(ns[0])], z["syms"])
     assert np.max(np.abs(syms[0, : 2 * int(ns[0])] - z["syms_libm"])) <= 1e-5
     b.close()
+    # the Costas NCO on glibc's own sin/cos: the libm fixture, bit for bit
+    b = Q.BatchDemodulator(1, Q.params(K.FS, K.FS // sps, K.ALPHA, span, max_samples_per_call=iq.size // 2,
+                                       costas_trig=1))
+    bits, nb, syms, ns = b.process(iq[None, :], want_syms=True)
+    assert Q.unpack_bits(bits[0], int(nb[0])) == bits_str(z["bits"])
+    assert np.array_equal(syms[0, : 2 * int(ns[0])], z["syms_libm"])
+    b.close()
 
 
 @pytest.mark.gpu
