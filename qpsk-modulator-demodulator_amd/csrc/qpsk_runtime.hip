@@ -37,6 +37,7 @@
 #include <cmath>
 #include <cstddef>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -179,6 +180,10 @@ struct qpsk_demod {
     uint64_t resident_issued = 0;    // workgroups of every gated loop launch so far
     uint64_t resident_gate = 0;      // what the newest gated loop launch brings it to, at least
     bool gate_pending = false;       // the next FIR has a loop launch to wait for
+    // off under a profiler's counter collection (rocprofv3 --pmc serialises
+    // every dispatch, and a stream parked on the wait then stalls the loop
+    // kernel it waits for) or with QPSK_PIPELINE_GATE=0
+    bool use_gate = true;
     int last_back = -1;              // boundary buffer of the newest back stage, -1 = none
     int64_t *h_len[2] = {nullptr, nullptr};   // pinned staging of per-call lengths
     // FLL on: the back stage (loop kernel) of the newest call is issued by the
@@ -558,6 +563,11 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
         h->wall_khz = 100000;
     if (h->loop_variant == 0 && h->lp.sps >= 8.0 && h->cus > 0 && (h->S + 23) / 24 <= h->cus / 2)
         h->loop_variant = 4;
+    {
+        const char *g = std::getenv("QPSK_PIPELINE_GATE");
+        const char *pmc = std::getenv("ROCPROF_COUNTER_COLLECTION");
+        h->use_gate = !((g && std::strcmp(g, "0") == 0) || (pmc && std::strcmp(pmc, "1") == 0));
+    }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipStreamCreate failed"));
     h->own_stream = true;
@@ -843,7 +853,8 @@ int process_async_one(qpsk_demod *h, const Call &c) {
             HIP_TRY(hipStreamWaitEvent(B, h->e_fll, 0));
             const int db = h->dbuf;
             h->deferred = false;
-            if ((rc = run_loop(h, dc, h->dlen, h->d_mf[db], B, h->dkt, h->d_resident))) return rc;
+            if ((rc = run_loop(h, dc, h->dlen, h->d_mf[db], B, h->dkt, h->use_gate ? h->d_resident : nullptr)))
+                return rc;
             HIP_TRY(hipEventRecord(h->e_back[db], B));
             h->back_rec[db] = true;
             h->last_back = db;
@@ -888,7 +899,7 @@ int process_async_one(qpsk_demod *h, const Call &c) {
         HIP_TRY(hipStreamWaitEvent(B, h->e_front[b], 0));
     }
     h->front_rec[b] = true;
-    if ((rc = run_loop(h, c, d_len, mf, B, kt, h->d_resident))) return rc;
+    if ((rc = run_loop(h, c, d_len, mf, B, kt, h->use_gate ? h->d_resident : nullptr))) return rc;
     HIP_TRY(hipEventRecord(h->e_back[b], B));
     h->back_rec[b] = true;
     h->last_back = b;

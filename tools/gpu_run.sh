@@ -42,7 +42,7 @@ for step in "$@"; do
       IFS=: read -r cfg kern algo <<< "$arg"
       for c in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv \
-          -d "$O/pmc_${c}_$cfg" -o run -- python3 "$R/bench.py" --config "$cfg" --steps 2 --warmup 1 \
+          -d "$O/pmc_${c}_$cfg" -o run -- python3 "$R/bench.py" --config "$cfg" --steps 2 --warmup 1 --serial-calls \
           --timed-only --sub-configs none > "$O/pmc_${c}_$cfg.log" 2>&1) || { tail -20 "$O/pmc_${c}_$cfg.log"; exit 1; }
       done
       python3 "$R/tools/pmc_traffic.py" --fetch "$O/pmc_FETCH_SIZE_$cfg" --write "$O/pmc_WRITE_SIZE_$cfg" \
