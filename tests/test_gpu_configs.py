@@ -126,3 +126,96 @@ def test_baseline_workload_seven_calls_vs_libm_oracle(key, trig):
                     assert np.array_equal(g, rsy), f"{key} stream {s} call {k}: symbols"
                 else:
                     assert np.max(np.abs(g - rsy), initial=0) <= SYM_TOL, f"{key} stream {s} call {k}"
+
+
+def _pipelined_rows(S, n, calls, sps, span, seed, idx, **kw):
+    """`calls` consecutive pipelined calls of n samples on a GPU-synthesised
+    batch; returns the host input rows idx and per call (bits, n_bits) of idx."""
+    import torch
+    dev = torch.device("cuda", 0)
+    iq, _ = Q.synth_generate(S, n * calls, K.FS, K.FS // sps, rrc_alpha=K.ALPHA, rrc_span=span, seed=seed,
+                             lo_ppm=1.0)
+    b = Q.BatchDemodulator(S, Q.params(K.FS, K.FS // sps, K.ALPHA, span, max_samples_per_call=n, **kw))
+    ms = b.max_symbols(n)
+    stream = torch.cuda.Stream(dev)
+    b.set_stream(stream.cuda_stream)
+    outs = []
+    torch.cuda.synchronize(dev)
+    for k in range(calls):
+        x = iq[:, 2 * n * k: 2 * n * (k + 1)].contiguous()
+        bits = torch.zeros((S, (2 * ms + 7) // 8 + 8), dtype=torch.uint8, device=dev)
+        nb = torch.zeros(S, dtype=torch.int64, device=dev)
+        b.process_device_async(x, n, bits, nb)
+        outs.append((x, bits, nb))
+    b.pipeline_wait()
+    torch.cuda.synchronize(dev)
+    host = _rows(iq, idx)
+    got = [(_rows(bits, idx), _rows(nb, idx)) for _, bits, nb in outs]
+    b.close()
+    return host, got
+
+
+def _oracle_calls(row, n, calls, sps, span):
+    d = K.oracle_for(sps, span)
+    return [d.demodulate_ex(row[2 * n * k: 2 * n * (k + 1)])[0] for k in range(calls)]
+
+
+def test_pipelined_loop_grid_larger_than_the_chip():
+    """12000 streams at sps 4: 375 loop workgroups, more than the 256 CUs hold
+    at once (one 125 KB workgroup each), so the residency gate the next FIR
+    waits on is the first dispatch wave, min(grid, CUs), not the whole grid;
+    the pipelined calls finish and match the oracle."""
+    S, n, calls = 12000, 4096, 3
+    idx = [0, 1, 5999, S - 2, S - 1]
+    host, got = _pipelined_rows(S, n, calls, 4, 32, 0x47415445, idx)
+    for j, s in enumerate(idx):
+        ref = _oracle_calls(host[j], n, calls, 4, 32)
+        for k in range(calls):
+            gb, gnb = got[k][0][j], got[k][1][j]
+            assert Q.unpack_bits(gb, int(gnb)) == ref[k], f"stream {s} call {k}"
+
+
+def test_pipelined_results_do_not_depend_on_the_gate(monkeypatch):
+    """QPSK_PIPELINE_GATE=0 (what a counter-collecting profiler gets) changes
+    only the dispatch order, not one bit."""
+    S, n, calls = 300, 8192, 4
+    idx = list(range(S))
+    _, with_gate = _pipelined_rows(S, n, calls, 8, 8, 0x51, idx)
+    monkeypatch.setenv("QPSK_PIPELINE_GATE", "0")
+    _, without = _pipelined_rows(S, n, calls, 8, 8, 0x51, idx)
+    for k in range(calls):
+        assert np.array_equal(with_gate[k][1], without[k][1])
+        for s in range(S):
+            nb = int(with_gate[k][1][s])
+            assert np.array_equal(with_gate[k][0][s][: (nb + 7) // 8], without[k][0][s][: (nb + 7) // 8])
+
+
+def test_two_pipelined_handles_interleaved():
+    """Two handles on one GPU, their pipelined calls interleaved: each has its
+    own residency counter and gate, and each matches the oracle."""
+    import torch
+    dev = torch.device("cuda", 0)
+    S, n, calls = 64, 8192, 3
+    iq, _ = Q.synth_generate(S, n * calls, K.FS, K.FS // 8, rrc_alpha=K.ALPHA, rrc_span=8, seed=77, lo_ppm=1.0)
+    hs = [Q.BatchDemodulator(S, Q.params(K.FS, K.FS // 8, K.ALPHA, 8, max_samples_per_call=n)) for _ in range(2)]
+    ms = hs[0].max_symbols(n)
+    outs = [[], []]
+    for k in range(calls):
+        x = iq[:, 2 * n * k: 2 * n * (k + 1)].contiguous()
+        for h, o in zip(hs, outs):
+            bits = torch.zeros((S, (2 * ms + 7) // 8 + 8), dtype=torch.uint8, device=dev)
+            nb = torch.zeros(S, dtype=torch.int64, device=dev)
+            h.process_device_async(x, n, bits, nb)
+            o.append((x, bits, nb))
+    for h in hs:
+        h.pipeline_wait()
+    torch.cuda.synchronize(dev)
+    host = iq[:4].cpu().numpy()
+    for s in range(4):
+        ref = _oracle_calls(host[s], n, calls, 8, 8)
+        for o in outs:
+            for k in range(calls):
+                _, bits, nb = o[k]
+                assert Q.unpack_bits(bits[s].cpu().numpy(), int(nb[s])) == ref[k], (s, k)
+    for h in hs:
+        h.close()
