@@ -552,7 +552,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
     torch.cuda.set_stream(stream)
     demod.set_stream(stream.cuda_stream)
     ms = demod.max_symbols(n)
-    bits = torch.zeros((S, (2 * ms + 7) // 8 + 64), dtype=torch.uint8, device=dev)
+    bits = torch.zeros((S, ((2 * ms + 7) // 8 + 127) // 64 * 64), dtype=torch.uint8, device=dev)
     nbits = torch.zeros(S, dtype=torch.int64, device=dev)
 
     # pipelined calls (qpsk_demod_process_async): call k+1's front stage (FIR,
@@ -710,7 +710,7 @@ def split_gather_leg(args, rank, world, dev, S=256):
     torch.cuda.set_stream(stream)
     demod.set_stream(stream.cuda_stream)
     ms = demod.max_symbols(n)
-    bits = torch.zeros((S, (2 * ms + 7) // 8 + 64), dtype=torch.uint8, device=dev)
+    bits = torch.zeros((S, ((2 * ms + 7) // 8 + 127) // 64 * 64), dtype=torch.uint8, device=dev)
     nbits = torch.zeros(S, dtype=torch.int64, device=dev)
 
     def synth(first, count):
@@ -753,7 +753,7 @@ def main():
                     help="comma list run after the headline as sub_records; 'auto' = c2,c4,c5 at N=1 "
                          "(c4: the per-GPU shard of BASELINE's 8-GPU config, the N = 1 point of its "
                          "curve), c4 at N>1; 'none' = headline only")
-    ap.add_argument("--sub-steps", type=int, default=5)
+    ap.add_argument("--sub-steps", type=int, default=20)
     ap.add_argument("--samples", type=int, default=1 << 20)
     ap.add_argument("--loop-variant", type=int, default=0,
                     help="symbol-loop kernel shape (qpsk_demod_params.loop_variant; 0 = auto)")

@@ -126,6 +126,11 @@ int qpsk_demod_set_stream(qpsk_demod *h, void *hip_stream);
  * return QPSK_ERR_STATE / QPSK_ERR_CAPACITY when they raised a QPSK_STATUS_*
  * flag (outputs are still written); device-memory calls report them through
  * qpsk_demod_status.
+ * Bytes of a bit row past the last bit (and floats of a symbol row past the
+ * last symbol) are unspecified.  Device rows that are 4-byte aligned with
+ * bits_stride_bytes % 4 == 0 (8-byte aligned, even syms_stride_floats for
+ * symbols) are written in place by the loop kernel, whole 32-bit words up to
+ * the row's last bit; other rows are filled from an internal buffer by a copy.
  */
 int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t stride_floats,
                        int64_t n_samples, const int64_t *lengths, int32_t mem, uint8_t *bits,

@@ -334,6 +334,29 @@ int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipS
     la.syms_stride = h->syms_cap;
     la.syms_cap = h->syms_cap;
     la.n_syms = h->d_counts + S;
+    // device-memory outputs whose rows the kernel can address as its own (4-B
+    // aligned word rows holding every word a row can take; float2-aligned
+    // symbol rows): written in place, no staging copy behind the kernel
+    const int64_t need_words = (2 * c.max_sym + 31) / 32;
+    const bool direct_bits = !c.append && c.mem == QPSK_MEM_DEVICE && la.bits && c.n_bits &&
+                             (reinterpret_cast<uintptr_t>(c.n_bits) & 7) == 0 &&
+                             (reinterpret_cast<uintptr_t>(c.bits) & 3) == 0 && (c.bits_stride_bytes & 3) == 0 &&
+                             c.bits_stride_bytes / 4 >= need_words;
+    const bool direct_syms = !c.append && c.mem == QPSK_MEM_DEVICE && c.syms &&
+                             (reinterpret_cast<uintptr_t>(c.syms) & 7) == 0 && (c.syms_stride_floats & 1) == 0 &&
+                             c.syms_stride_floats / 2 >= c.max_sym;
+    if (direct_bits) {
+        la.bits = reinterpret_cast<uint32_t *>(c.bits);
+        la.bits_stride_words = c.bits_stride_bytes / 4;
+        la.bits_cap_words = c.bits_stride_bytes / 4;
+        la.n_bits = c.n_bits;
+    }
+    if (direct_syms) {
+        la.syms = c.syms;
+        la.syms_stride = c.syms_stride_floats / 2;
+        la.syms_cap = c.syms_stride_floats / 2;
+        if (c.n_syms && (reinterpret_cast<uintptr_t>(c.n_syms) & 7) == 0) la.n_syms = c.n_syms;
+    }
     la.S = S;
     // host-memory calls (chunks of one included) raise into slot 1, which the
     // call clears first and reads back at its end; device-memory calls into
@@ -380,9 +403,9 @@ int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipS
     }
     const hipMemcpyKind kind = c.mem == QPSK_MEM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
     const int64_t bytes_row = (2 * c.max_sym + 7) / 8;
-    if (c.bits && bytes_row > 0)
+    if (c.bits && bytes_row > 0 && !direct_bits)
         HIP_TRY(hipMemcpy2DAsync(c.bits, c.bits_stride_bytes, h->d_bits, h->bits_words * 4, bytes_row, S, kind, st));
-    if (c.syms && c.max_sym > 0)
+    if (c.syms && c.max_sym > 0 && !direct_syms)
         HIP_TRY(hipMemcpy2DAsync(c.syms, c.syms_stride_floats * sizeof(float), h->d_syms,
                                  2 * h->syms_cap * sizeof(float), 2 * c.max_sym * sizeof(float), S, kind, st));
     if (c.mem == QPSK_MEM_HOST) {
@@ -393,8 +416,9 @@ int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipS
         if (c.n_syms) std::memcpy(c.n_syms, h->h_counts + S, S * sizeof(int64_t));
         h->status_host |= *h->h_flags;
     } else {
-        if (c.n_bits) HIP_TRY(hipMemcpyAsync(c.n_bits, h->d_counts, S * sizeof(int64_t), kind, st));
-        if (c.n_syms) HIP_TRY(hipMemcpyAsync(c.n_syms, h->d_counts + S, S * sizeof(int64_t), kind, st));
+        if (c.n_bits && !direct_bits) HIP_TRY(hipMemcpyAsync(c.n_bits, h->d_counts, S * sizeof(int64_t), kind, st));
+        if (c.n_syms && !(direct_syms && la.n_syms == c.n_syms))
+            HIP_TRY(hipMemcpyAsync(c.n_syms, h->d_counts + S, S * sizeof(int64_t), kind, st));
     }
     return QPSK_OK;
 }

@@ -261,11 +261,28 @@ def test_synth_generated_batch_parity_and_ber():
     assert clean >= S // 2
 
 
-def async_run(iq2d, calls, sps, span, sync_every=0, **kw):
+def out_rows(S, ms, layout):
+    """Device output rows.  "direct": word-aligned rows the loop kernel writes
+    in place; "staged": a 1-byte-offset bit row of odd stride and an odd
+    symbol stride, which take the staging buffers and the 2-D copies."""
+    import torch
+    if layout == "staged":
+        bw = (2 * ms + 7) // 8 + 9
+        bw += 1 - bw % 2
+        bits = torch.zeros((S, bw + 1), dtype=torch.uint8, device="cuda")[:, 1:]
+        sy = torch.zeros((S, 2 * ms + 1), dtype=torch.float32, device="cuda")
+    else:
+        bits = torch.zeros((S, ((2 * ms + 7) // 8 + 63) // 64 * 64), dtype=torch.uint8, device="cuda")
+        sy = torch.zeros((S, 2 * ms), dtype=torch.float32, device="cuda")
+    return bits, sy
+
+
+def async_run(iq2d, calls, sps, span, sync_every=0, layout=None, **kw):
     """The same call sequence through qpsk_demod_process_async (front stage of
     call k+1 overlapping the back stage of call k), every call's outputs in
     their own device rows, one pipeline_wait at the end.  sync_every > 0 makes
-    every sync_every-th call a synchronous process() (mixed ordering)."""
+    every sync_every-th call a synchronous process() (mixed ordering).
+    layout: None (rows as a caller would size them), or out_rows' layouts."""
     import torch
     S = iq2d.shape[0]
     nmax = max(max(c) for c in calls)
@@ -283,9 +300,12 @@ def async_run(iq2d, calls, sps, span, sync_every=0, **kw):
             for s in range(S):
                 x[s, : 2 * lens[s]] = iq2d[s, 2 * pos[s]: 2 * (pos[s] + lens[s])]
             xd = torch.from_numpy(x).to("cuda", non_blocking=False)
-            bits = torch.zeros((S, (2 * ms + 7) // 8 + 8), dtype=torch.uint8, device="cuda")
+            if layout:
+                bits, sy = out_rows(S, ms, layout)
+            else:
+                bits = torch.zeros((S, (2 * ms + 7) // 8 + 8), dtype=torch.uint8, device="cuda")
+                sy = torch.zeros((S, 2 * ms), dtype=torch.float32, device="cuda")
             nb = torch.zeros(S, dtype=torch.int64, device="cuda")
-            sy = torch.zeros((S, 2 * ms), dtype=torch.float32, device="cuda")
             ns = torch.zeros(S, dtype=torch.int64, device="cuda")
             uniform = all(l == lens[0] for l in lens)
             if sync_every and ci % sync_every == sync_every - 1:
@@ -305,6 +325,19 @@ def async_run(iq2d, calls, sps, span, sync_every=0, **kw):
         res.append([(Q.unpack_bits(bits[s], int(nb[s])), sy[s, : 2 * int(ns[s])].copy()) for s in range(S)])
     b.close()
     return res, depth
+
+
+@pytest.mark.parametrize("layout", ["direct", "staged"])
+@pytest.mark.parametrize("sync_every", [0, 2])
+def test_device_output_rows_in_place_or_staged(layout, sync_every):
+    """Device calls whose rows the loop kernel can address are written in
+    place (no 2-D copy behind it); misaligned or odd-stride rows go through
+    the staging buffers.  Both, synchronous and pipelined, equal the oracle."""
+    iq = K.batch_signals(4, seed0=470, sps=8, span=8, n_bits=2400, snr_db=16)
+    n = iq.shape[1] // 2
+    calls = [[n // 4] * 4, [n // 3] * 4, [n // 5] * 4, [n - n // 4 - n // 3 - n // 5] * 4]
+    got, _ = async_run(iq, calls, 8, 8, sync_every=sync_every, layout=layout)
+    assert_same(got, oracle_run(iq, calls, 8, 8))
 
 
 @pytest.mark.parametrize("fll", [False, True])
