@@ -20,12 +20,12 @@
 // Device layout (HBM, stream-major so every stage reads/writes each stream's
 // time axis contiguously):
 //   in      [S][n_max]              float2  staging for host input
-//   fll_out [2][S][n_max]           float2  (FLL mode; the 2nd only when pipelined)
+//   fll_out [S][n_max]              float2  (FLL mode)
 //   hist    2 x [S][T-1]            float2  FIR delay line (ping-pong)
-//   mf      [2][S][64 + n_max]      float2  matched-filter output; the 64-slot
+//   mf      [2][S][256 + n_max]     float2  matched-filter output; the 256-slot
 //                                           prefix receives the M&M carry (the
-//                                           2nd only when pipelined, FLL off)
-//   carry   [S][64]                 float2  M&M retained samples
+//                                           2nd only when pipelined)
+//   carry   [S][256]                float2  M&M retained samples
 //   state   [S]                     StreamState
 //   bits    [S][words]              uint32  MSB-first packed bits
 //   syms    [S][syms_cap]           float2  rotated symbols (on request)
@@ -949,7 +949,7 @@ int flush_deferred(qpsk_demod *h) {
 int host_call_status(qpsk_demod *h) {
     const uint32_t f = *h->h_flags;
     if (f & QPSK_STATUS_CARRY_OVERFLOW)
-        return fail(QPSK_ERR_STATE, "symbol-sync queue over 64 retained samples (sps > 60?)");
+        return fail(QPSK_ERR_STATE, "symbol-sync queue over 256 retained samples (sps > 250?)");
     if (f & QPSK_STATUS_OUTPUT_TRUNCATED) return fail(QPSK_ERR_CAPACITY, "output row truncated");
     if (f & QPSK_STATUS_NONFINITE_TIMING)
         return fail(QPSK_ERR_STATE, "non-finite sample reached the symbol timing loop");

@@ -15,8 +15,10 @@
 
 namespace qpsk {
 
-constexpr int kCarryMax = 64;      // retained M&M samples between calls (normally 3)
-constexpr int kMfPrefix = 64;      // MF buffer prefix that receives the carry
+// retained M&M samples between calls: normally sps + 3 at most (the samples
+// from the next symbol's base on), so 256 covers sps up to ~250
+constexpr int kCarryMax = 256;
+constexpr int kMfPrefix = 256;     // MF buffer prefix that receives the carry
 constexpr int kFllTaps = 40;       // QPSKDeModulator.cs:35
 
 struct alignas(16) StreamState {

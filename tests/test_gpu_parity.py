@@ -114,6 +114,24 @@ def test_chunked_ragged_calls_bit_exact(sps, span, variant):
     assert_same(gpu_run(iq, calls, sps, span, loop_variant=variant), oracle_run(iq, calls, sps, span))
 
 
+@pytest.mark.parametrize("sps,span", [(30, 6), (100, 4), (200, 2)])
+def test_large_sps_multi_call_bit_exact(sps, span):
+    """Samples per symbol up to 200 (the reference's own testFullDemodChain
+    runs sps 30): the M&M queue retained between calls (up to sps + 3
+    samples, MuellerMuller.cs:123-133) rides in the 256-sample carry, across
+    calls shorter than one symbol too."""
+    iq = K.batch_signals(3, seed0=25, sps=sps, span=span, n_bits=300, snr_db=18)
+    n = iq.shape[1] // 2
+    calls, left, k = [], np.full(3, n), 0
+    sizes = [1, 7, sps // 2, 3 * sps + 5, 0, 2 * sps - 1, 4096]
+    while left.max() > 0:
+        c = [int(min(left[s], sizes[(k + s) % len(sizes)])) for s in range(3)]
+        calls.append(c)
+        left -= np.array(c)
+        k += 1
+    assert_same(gpu_run(iq, calls, sps, span), oracle_run(iq, calls, sps, span))
+
+
 def test_empty_call_keeps_state():
     iq = K.batch_signals(2, seed0=30, n_bits=1200)
     n = iq.shape[1] // 2
