@@ -272,6 +272,35 @@ def portable_check(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, idx, costa
     return len(bad), sym_bad
 
 
+def steady_state_check(iq, bits_dev, nbits_dev, cfg, idx, calls):
+    """The timed region's own output: the bit rows of streams idx after the
+    handle's `calls` consecutive calls on the same input buffer (warmup +
+    timed steps), against the libm oracle fed the same call sequence.  The
+    bench re-feeds one buffer, so the streams are discontinuous at every call
+    and some Costas loops sit in false lock with theta growing call by call:
+    the state the timed region actually runs in, which the fresh-state legs
+    do not reach.  Returns (mismatching streams, first mismatches)."""
+    from concurrent.futures import ThreadPoolExecutor
+    import qpsk_amd as Q
+    import oracle as O
+    host = rows_to_host(iq, idx)
+    gb = rows_to_host(bits_dev, idx)
+    gnb = rows_to_host(nbits_dev, idx)
+
+    def one(i):
+        d = O.OracleDemod(FS, FS // cfg["sps"], ALPHA, cfg["span"], enable_fll=cfg["fll"],
+                          trig=O.TRIG_LIBM, ring_capacity=4096)
+        for _ in range(calls - 1):
+            d.demodulate_ex(host[i])
+        ref, _, _ = d.demodulate_ex(host[i])
+        return ref == Q.unpack_bits(gb[i], int(gnb[i]))
+
+    with ThreadPoolExecutor(max_workers=len(idx)) as ex:
+        same = list(ex.map(one, range(len(idx))))
+    bad = [idx[i] for i, ok in enumerate(same) if not ok]
+    return len(bad), bad[:8]
+
+
 def ber_after_lock(bits_dev, nbits_dev, tx_dev, n_streams, skip_bits=8000, window=2048,
                    key_bits=64, search=512):
     """Bit errors after acquisition, with windowed realignment.
@@ -524,6 +553,7 @@ def rooflines(st, S, n, cfg, lt=None):
 # one configuration
 # ---------------------------------------------------------------------------
 def run_config(key, args, rank, world, dev, steps, warmup, headline):
+    import numpy as np
     import torch
     import torch.distributed as dist
     import qpsk_amd as Q
@@ -593,6 +623,18 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
     errs = total_bits = lost = slips = 0
     bad_bits = bad_syms = n_port = 0
     libm_bad = libm_streams = 0
+    steady_bad = steady_n = 0
+    steady_ex, steady_freq = [], []
+    if not args.timed_only and not args.no_parity:
+        # the last timed call's rows, before anything overwrites them: the first
+        # and last two streams and the four whose Costas loop runs fastest (the
+        # false locks, theta growing call by call: the hardest state to track)
+        fr = np.abs(demod.stream_states()["freq"])
+        hot = [int(i) for i in np.argsort(-fr, kind="stable")[:4]]
+        sidx = sorted(set(([0, 1, S - 2, S - 1] if S >= 4 else list(range(S))) + hot))
+        steady_freq = [round(float(fr[i]), 4) for i in hot]
+        steady_bad, steady_ex = steady_state_check(iq, bits, nbits, cfg, sidx, warmup + steps)
+        steady_n = len(sidx)
     if not args.timed_only:
         # untimed: one call from the initial state on every stream of the timed
         # handle (stream starts at t=0); its rows feed parity and BER
@@ -622,8 +664,10 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
                 if rank == 0:
                     rec["cpu_baseline"], rec["parity_vs_libm_oracle"] = cpu, par
         del syms, nsyms
-    t_max, (errs, total_bits, lost, slips, bad_bits, bad_syms, n_port, libm_bad, libm_streams) = reduce_stats(
-        elapsed, [errs, total_bits, lost, slips, bad_bits, bad_syms, n_port, libm_bad, libm_streams],
+    t_max, (errs, total_bits, lost, slips, bad_bits, bad_syms, n_port, libm_bad, libm_streams,
+            steady_bad, steady_n) = reduce_stats(
+        elapsed, [errs, total_bits, lost, slips, bad_bits, bad_syms, n_port, libm_bad, libm_streams,
+                  steady_bad, steady_n],
         device=dev if nccl else None)
     if world > 1 and "parity_vs_libm_oracle" in rec:
         par = rec["parity_vs_libm_oracle"]
@@ -673,6 +717,15 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
                            "ber": (errs / total_bits) if total_bits else None,
                            "lost_windows": lost, "symbol_slips": slips,
                            "streams": min(S, 32) * world},
+        "parity_steady_state": (
+            "not checked" if (args.no_parity or args.timed_only) else
+            {"streams": steady_n, "mismatching_streams": steady_bad, "calls": warmup + steps,
+             "oracle": "CPU oracle, glibc trig, fed the same call sequence",
+             "mismatch_examples_rank0": steady_ex,
+             "fastest_costas_freq_rank0": steady_freq,
+             "note": "bits of the timed region's last call after every warmup and timed call on "
+                     "the one input buffer: the first and last two streams of every rank's shard and "
+                     "the four with the largest |Costas freq| (false locks, rad/symbol)"}),
         "parity_vs_portable_oracle": (
             "not checked" if (args.no_parity or args.timed_only) else
             {"streams": n_port, "bit_mismatch_streams": bad_bits, "symbol_mismatch_streams": bad_syms,

@@ -279,6 +279,15 @@ def pack_bits(bits: str) -> np.ndarray:
     return np.packbits(a)
 
 
+# StreamState (csrc/qpsk_state.h), the head of a qpsk_demod_get_state blob
+STREAM_STATE_DTYPE = np.dtype([("mu", "f8"), ("integ", "f8"), ("theta", "f8"), ("freq", "f8"),
+                               ("base", "i4"), ("has_prev", "i4"), ("psi", "f4"), ("psq", "f4"),
+                               ("pdi", "f4"), ("pdq", "f4"), ("carry_n", "i4"), ("diff_have", "i4"),
+                               ("diff_pi", "f4"), ("diff_pq", "f4"), ("fll_phase", "f4"),
+                               ("fll_freq", "f4"), ("fll_pos", "i4"), ("error", "i4"), ("tofs", "i8"),
+                               ("iqb_re", "f4"), ("iqb_im", "f4"), ("_pad", "V8")])   # alignas(16): 112 B
+
+
 class BatchDemodulator:
     """A batch of S independent reference demodulators on one MI355X."""
 
@@ -357,6 +366,12 @@ class BatchDemodulator:
         buf = C.create_string_buffer(n)
         _check(lib().qpsk_demod_get_state(self._h, buf))
         return buf.raw
+
+    def stream_states(self, blob: bytes | None = None) -> np.ndarray:
+        """The per-stream loop state records (StreamState, csrc/qpsk_state.h)
+        at the head of a get_state() blob, as a structured array [S]."""
+        blob = self.get_state() if blob is None else blob
+        return np.frombuffer(blob[: self.S * STREAM_STATE_DTYPE.itemsize], dtype=STREAM_STATE_DTYPE)
 
     def set_state(self, blob: bytes):
         buf = C.create_string_buffer(blob, len(blob))

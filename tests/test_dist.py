@@ -172,3 +172,28 @@ def test_bench_gpus_flag_must_match_world_size():
     r = subprocess.run([sys.executable, os.path.join(K_ROOT, "bench.py"), "--gpus", "2"],
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in (r.stderr + r.stdout)
+
+
+def test_steady_state_check_replays_the_call_sequence():
+    """bench.steady_state_check feeds the oracle the same buffer `calls` times
+    and compares the last call's bits with the handle's rows: rows built from
+    that replay pass, one flipped bit is reported by stream."""
+    import qpsk_amd as Q
+    iq = K.batch_signals(4, seed0=5, sps=8, span=8, n_bits=1500, snr_db=16)
+    calls = 3
+    rows, nbits = [], []
+    for s in range(4):
+        d = O.OracleDemod(K.FS, K.FS // 8, K.ALPHA, 8, trig=O.TRIG_LIBM, ring_capacity=4096)
+        for _ in range(calls):
+            b, _, _ = d.demodulate_ex(iq[s])
+        rows.append(np.asarray(Q.pack_bits(b)))
+        nbits.append(len(b))
+    nb = torch.tensor(nbits, dtype=torch.int64)
+    bits = torch.zeros((4, max(r.size for r in rows) + 8), dtype=torch.uint8)
+    for s, r in enumerate(rows):
+        bits[s, : r.size] = torch.from_numpy(r)
+    cfg = dict(bench.CONFIGS["c2"])
+    assert bench.steady_state_check(torch.from_numpy(iq), bits, nb, cfg, [0, 1, 2, 3], calls) == (0, [])
+    assert bench.steady_state_check(torch.from_numpy(iq), bits, nb, cfg, [0, 1, 2, 3], calls - 1)[0] > 0
+    bits[2, 3] ^= 1
+    assert bench.steady_state_check(torch.from_numpy(iq), bits, nb, cfg, [0, 1, 2, 3], calls) == (1, [2])

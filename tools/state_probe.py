@@ -15,13 +15,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "qpsk-modulator-demodulator_amd"))
 sys.path.insert(0, ROOT)
 
-STATE = np.dtype([("mu", "f8"), ("integ", "f8"), ("theta", "f8"), ("freq", "f8"), ("base", "i4"),
-                  ("has_prev", "i4"), ("psi", "f4"), ("psq", "f4"), ("pdi", "f4"), ("pdq", "f4"),
-                  ("carry_n", "i4"), ("diff_have", "i4"), ("diff_pi", "f4"), ("diff_pq", "f4"),
-                  ("fll_phase", "f4"), ("fll_freq", "f4"), ("fll_pos", "i4"), ("error", "i4"),
-                  ("tofs", "i8"), ("iqb_re", "f4"), ("iqb_im", "f4"),
-                  ("_pad", "V8")])   # alignas(16): sizeof(StreamState) == 112
-
 
 def main():
     ap = argparse.ArgumentParser()
@@ -54,7 +47,7 @@ def main():
         torch.cuda.synchronize()
         t = d.stage_times()
         d.enable_timing(False)
-        s = np.frombuffer(d.get_state()[: S * STATE.itemsize], dtype=STATE)
+        s = d.stream_states()
         th, fr = np.abs(s["theta"]), np.abs(s["freq"])
         rec = {"call": c, "fll_ms": round(t.get("fll", 0.0), 2), "fir_ms": round(t["fir"], 2), "loop_ms": round(t["loop"], 2),
                "theta_gt_1e6": int((th > 1e6).sum()), "theta_gt_2p40": int((th > 2.0 ** 40).sum()),
