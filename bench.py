@@ -501,10 +501,11 @@ def launch_stats(col):
             "ms_std": round(float(v.std()), 4), "slow_launches": int((v > 1.3 * med).sum())}
 
 
-def rooflines(st, S, n, cfg, lt=None):
+def rooflines(st, S, n, cfg, lt=None, fir_ghz=None):
     """Per-kernel rooflines of the timed region (algorithmic
     bytes / flops per unit ÷ the kernel's mean launch time from the in-kernel
-    timestamps).  lt: launch_times() rows of the timed calls."""
+    timestamps).  lt: launch_times() rows of the timed calls; fir_ghz: the
+    shader clock each timed FIR ran at (fir_clocks())."""
     sps, T = cfg["sps"], cfg["span"] * cfg["sps"] + 1
     out = {}
     col = {"fll": 0, "fir": 1, "loop": 2}
@@ -522,6 +523,16 @@ def rooflines(st, S, n, cfg, lt=None):
                       "valu_frac_unfused": round(tfl / FP32_PEAK_UNFUSED_TFLOPS, 4),
                       "per_unit": f"16 B and {4 * T} flop per complex sample, {S * n} samples per launch",
                       "launch_stats": stats["fir"]}
+        clk = [float(v) for v in (fir_ghz if fir_ghz is not None else []) if v > 0]
+        if clk:
+            # the unfused VALU peak at the clock the FIR actually ran at: 78.65
+            # TFLOP/s is quoted at 2.4 GHz
+            g = sorted(clk)[len(clk) // 2]
+            out["fir"]["clock_ghz_median"] = round(g, 3)
+            out["fir"]["clock_ghz_range"] = [round(min(clk), 3), round(max(clk), 3)]
+            out["fir"]["valu_frac_unfused_at_clock"] = round(tfl / (FP32_PEAK_UNFUSED_TFLOPS * g / 2.4), 4)
+            out["fir"]["clock_source"] = ("s_memtime / s_memrealtime over the lifetimes of every "
+                                          "64th FIR workgroup, per launch")
     if st["loop"] > 0:
         loop_s = st["loop"] / 1e3
         b = (8.0 + 0.25 / sps) * S * n               # MF samples in + packed bits out
@@ -617,6 +628,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
     elapsed = time.perf_counter() - t0
     st = demod.stage_times()
     lt = demod.launch_times()
+    fir_ghz = demod.fir_clocks()
     demod.enable_timing(False)
 
     rec = {}
@@ -679,7 +691,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
                         f"summed over {world} ranks")
 
     value = world * S * n * steps / t_max / 1e6
-    rl = rooflines(st, S, n, cfg, lt)
+    rl = rooflines(st, S, n, cfg, lt, fir_ghz)
     dom = max(rl, key=lambda k: rl[k]["ms"]) if rl else None
     roof = None
     if dom:
@@ -687,6 +699,8 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
         roof = {"bound": r["bound"], "kernel": r["kernel"], "achieved": r["achieved"], "peak": r["peak"],
                 "unit": r["unit"], "frac": r["frac"], "valu_frac": r.get("valu_frac"),
                 "valu_frac_unfused": r.get("valu_frac_unfused"),
+                "clock_ghz": r.get("clock_ghz_median"),
+                "valu_frac_unfused_at_clock": r.get("valu_frac_unfused_at_clock"),
                 "traffic": (load_traffic(key) if dom == "fir" and S == cfg["streams"] and n == 1 << 20
                             else None)}
     rec = {

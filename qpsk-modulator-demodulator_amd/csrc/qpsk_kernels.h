@@ -36,7 +36,11 @@ struct FirArgs {
     int64_t y_stride;
     int64_t y_offset;
     unsigned long long *kt;   // launch timestamps or nullptr
+    // or nullptr: {sum of shader-clock ticks, sum of wall ticks} over the
+    // lifetimes of every kFirClockEvery-th workgroup (the clock the FIR runs at)
+    unsigned long long *clk;
 };
+constexpr unsigned kFirClockEvery = 64;
 
 struct LoopArgs {
     float *mf;             // [S][mf_stride] float2, MF output at kMfPrefix

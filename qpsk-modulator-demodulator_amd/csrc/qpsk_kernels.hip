@@ -212,6 +212,13 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, const float *hr
         if (kt_last) kt_end(a.kt);
         return;
     }
+    // shader-clock sample: this workgroup's lifetime in both clocks
+    const bool clk_wg = a.clk && tid == 0 && lin % kFirClockEvery == 0;
+    unsigned long long c0 = 0, r0 = 0;
+    if (clk_wg) {
+        c0 = __builtin_amdgcn_s_memtime();
+        r0 = wall_clock64();
+    }
     const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
     const f2 *hist = reinterpret_cast<const f2 *>(a.hist) + static_cast<int64_t>(s) * (T - 1);
 
@@ -263,6 +270,11 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, const float *hr
             };
             y[go] = fir_exact_one(xs, hrev, T, W);
         }
+    }
+    if (clk_wg) {
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = wall_clock64();
+        atomicAdd(a.clk, c1 - c0);
+        atomicAdd(a.clk + 1, r1 - r0);
     }
     if (kt_last) kt_end(a.kt);
 }

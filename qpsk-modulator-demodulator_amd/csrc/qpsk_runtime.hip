@@ -306,9 +306,11 @@ int run_fir(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_le
     fa.lengths = d_len; fa.n = n_call;
     fa.y = mf; fa.y_stride = h->mf_stride; fa.y_offset = kMfPrefix;
     fa.kt = kt ? kt + 2 : nullptr;
+    fa.clk = kt ? kt + 6 : nullptr;
     if (n_call > 0) {
         launch_fir(fa, h->d_hrev, h->T, h->W, h->S, n_call, st);
         fa.kt = nullptr;
+        fa.clk = nullptr;
         launch_fir_hist(fa, h->d_hist[h->hist_cur ^ 1], h->T - 1, h->S, st);
         h->hist_cur ^= 1;
     }
@@ -703,9 +705,11 @@ int qpsk_demod_enable_timing(qpsk_demod *h, int32_t on) {
     int rc;
     const size_t n = static_cast<size_t>(kKtCalls) * kKtPerCall;
     if (!h->d_kt && (rc = dev_alloc(&h->d_kt, n))) return rc;
-    // (start, end) pairs: start = +inf for the atomic minimum, end = 0 for the maximum
+    // (start, end) pairs of slots 0-5: start = +inf for the atomic minimum, end
+    // = 0 for the maximum; slots 6-7 (FIR clock sums) = 0
     std::vector<unsigned long long> init(n, 0ull);
-    for (size_t i = 0; i < n; i += 2) init[i] = ~0ull;
+    for (size_t i = 0; i < n; i += 2)
+        if (i % kKtPerCall < 6) init[i] = ~0ull;
     if ((rc = drain_async(h))) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
     HIP_TRY(hipMemcpy(h->d_kt, init.data(), n * sizeof(unsigned long long), hipMemcpyHostToDevice));
@@ -756,6 +760,25 @@ int qpsk_demod_stage_times(qpsk_demod *h, float *ms, int32_t n) {
                 ++cnt;
             }
         ms[i] = cnt ? static_cast<float>(sum / cnt) : 0.f;
+    }
+    return k;
+}
+
+int qpsk_demod_fir_clocks(qpsk_demod *h, float *ghz, int32_t max_calls) {
+    if (!h || !ghz) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    if (!h->kt_used) return 0;
+    int rc;
+    if ((rc = drain_async(h))) return rc;
+    HIP_TRY(hipSetDevice(h->p.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (h->s_front) HIP_TRY(hipStreamSynchronize(h->s_front));
+    if (h->s_back) HIP_TRY(hipStreamSynchronize(h->s_back));
+    std::vector<unsigned long long> t(static_cast<size_t>(h->kt_used) * kKtPerCall);
+    HIP_TRY(hipMemcpy(t.data(), h->d_kt, t.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    const int k = std::min<int32_t>(max_calls, h->kt_used);
+    for (int c = 0; c < k; ++c) {
+        const unsigned long long *s = t.data() + static_cast<size_t>(kKtPerCall) * c;
+        ghz[c] = s[7] ? static_cast<float>(static_cast<double>(s[6]) / s[7] * h->wall_khz * 1e-6) : 0.f;
     }
     return k;
 }
