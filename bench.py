@@ -501,15 +501,30 @@ def launch_stats(col):
             "ms_std": round(float(v.std()), 4), "slow_launches": int((v > 1.3 * med).sum())}
 
 
-def rooflines(st, S, n, cfg, lt=None, fir_ghz=None):
+def rooflines(st, S, n, cfg, lt=None, kclk=None):
     """Per-kernel rooflines of the timed region (algorithmic
     bytes / flops per unit ÷ the kernel's mean launch time from the in-kernel
-    timestamps).  lt: launch_times() rows of the timed calls; fir_ghz: the
-    shader clock each timed FIR ran at (fir_clocks())."""
+    timestamps).  lt: launch_times() rows of the timed calls; kclk:
+    kernel_clocks() rows (the shader clock each kernel ran at, GHz)."""
     sps, T = cfg["sps"], cfg["span"] * cfg["sps"] + 1
     out = {}
     col = {"fll": 0, "fir": 1, "loop": 2}
     stats = {k: (launch_stats(lt[:, i]) if lt is not None and len(lt) else None) for k, i in col.items()}
+
+    def clock(k):
+        if kclk is None or not len(kclk):
+            return None
+        v = sorted(float(x) for x in kclk[:, col[k]] if x > 0)
+        return (v[len(v) // 2], v[0], v[-1]) if v else None
+
+    def add_clock(k, extra):
+        c = clock(k)
+        if c and k in out:
+            out[k]["clock_ghz_median"] = round(c[0], 3)
+            out[k]["clock_ghz_range"] = [round(c[1], 3), round(c[2], 3)]
+            out[k].update(extra(c[0]))
+            out[k]["clock_source"] = ("s_memtime / s_memrealtime over sampled wave lifetimes of every "
+                                      "timed launch (qpsk_demod_kernel_clocks)")
     if st["fir"] > 0:
         fir_s = st["fir"] / 1e3
         gbs = 16.0 * S * n / fir_s / 1e9             # 8 B in + 8 B out per complex sample
@@ -523,16 +538,10 @@ def rooflines(st, S, n, cfg, lt=None, fir_ghz=None):
                       "valu_frac_unfused": round(tfl / FP32_PEAK_UNFUSED_TFLOPS, 4),
                       "per_unit": f"16 B and {4 * T} flop per complex sample, {S * n} samples per launch",
                       "launch_stats": stats["fir"]}
-        clk = [float(v) for v in (fir_ghz if fir_ghz is not None else []) if v > 0]
-        if clk:
-            # the unfused VALU peak at the clock the FIR actually ran at: 78.65
-            # TFLOP/s is quoted at 2.4 GHz
-            g = sorted(clk)[len(clk) // 2]
-            out["fir"]["clock_ghz_median"] = round(g, 3)
-            out["fir"]["clock_ghz_range"] = [round(min(clk), 3), round(max(clk), 3)]
-            out["fir"]["valu_frac_unfused_at_clock"] = round(tfl / (FP32_PEAK_UNFUSED_TFLOPS * g / 2.4), 4)
-            out["fir"]["clock_source"] = ("s_memtime / s_memrealtime over the lifetimes of every "
-                                          "64th FIR workgroup, per launch")
+        # the unfused VALU peak at the clock the FIR actually ran at (78.65
+        # TFLOP/s is quoted at 2.4 GHz)
+        add_clock("fir", lambda g: {"valu_frac_unfused_at_clock":
+                                    round(tfl / (FP32_PEAK_UNFUSED_TFLOPS * g / 2.4), 4)})
     if st["loop"] > 0:
         loop_s = st["loop"] / 1e3
         b = (8.0 + 0.25 / sps) * S * n               # MF samples in + packed bits out
@@ -545,6 +554,9 @@ def rooflines(st, S, n, cfg, lt=None, fir_ghz=None):
                        "per_unit": f"{8 + 0.25 / sps:.4f} B per complex sample, {S * n} samples, "
                                    f"{int(syms)} symbols per launch",
                        "launch_stats": stats["loop"]}
+        # shader cycles per symbol of one stream's chain (the stamped loop
+        # probe's figure of merit)
+        add_clock("loop", lambda g: {"cycles_per_symbol": round(loop_s * g * 1e9 / (n / sps), 1)})
     if cfg["fll"] and st["fll"] > 0:
         fll_s = st["fll"] / 1e3
         tfl = 640.0 * S * n / fll_s / 1e12
@@ -555,6 +567,9 @@ def rooflines(st, S, n, cfg, lt=None, fir_ghz=None):
                       "valu_tflops": round(tfl, 2), "valu_frac": round(tfl / FP32_PEAK_TFLOPS, 4),
                       "per_unit": "16 B and 640 flop (+ one sincos) per complex sample",
                       "launch_stats": stats["fll"]}
+        # shader cycles per sample of a wave (8 streams x 8 lanes): against
+        # its instruction count per sample, the wave's issue rate
+        add_clock("fll", lambda g: {"cycles_per_sample": round(fll_s * g * 1e9 / n, 1)})
     for v in out.values():
         v["source"] = TIMING_SOURCE
     return out
@@ -628,7 +643,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
     elapsed = time.perf_counter() - t0
     st = demod.stage_times()
     lt = demod.launch_times()
-    fir_ghz = demod.fir_clocks()
+    kclk = demod.kernel_clocks()
     demod.enable_timing(False)
 
     rec = {}
@@ -691,7 +706,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
                         f"summed over {world} ranks")
 
     value = world * S * n * steps / t_max / 1e6
-    rl = rooflines(st, S, n, cfg, lt, fir_ghz)
+    rl = rooflines(st, S, n, cfg, lt, kclk)
     dom = max(rl, key=lambda k: rl[k]["ms"]) if rl else None
     roof = None
     if dom:

@@ -195,13 +195,15 @@ int64_t qpsk_tsc_find(const uint8_t *bits, int64_t n_bits, const char *tsc);
  * run counts as absent.  Returns the number of entries written (<= 4).
  * launch_times: the same four values per call, ms[4*k .. 4*k+3] for call k
  * (0 = did not run); returns the number of calls written (<= max_calls).
- * fir_clocks: per recorded call, the shader clock (GHz) the matched-filter
- * FIR ran at: shader-clock ticks (s_memtime) over wall ticks of a sample of
- * its workgroups' lifetimes (0 = no sample); returns the calls written. */
+ * kernel_clocks: per recorded call, the shader clock (GHz) the FLL, the FIR
+ * and the loop kernel ran at, ghz[3*k .. 3*k+2]: shader-clock ticks
+ * (s_memtime) over wall ticks of a sample of their waves' lifetimes (FIR:
+ * every 64th workgroup; FLL: every workgroup; loop: every M&M wave; 0 = did
+ * not run); returns the calls written. */
 int qpsk_demod_enable_timing(qpsk_demod *h, int32_t on);
 int qpsk_demod_stage_times(qpsk_demod *h, float *ms, int32_t n);
 int qpsk_demod_launch_times(qpsk_demod *h, float *ms, int32_t max_calls);
-int qpsk_demod_fir_clocks(qpsk_demod *h, float *ghz, int32_t max_calls);
+int qpsk_demod_kernel_clocks(qpsk_demod *h, float *ghz, int32_t max_calls);
 
 /* Design products, for parity checks against the reference constructor. */
 int qpsk_demod_rrc_taps(const qpsk_demod *h, float *taps, int32_t cap);

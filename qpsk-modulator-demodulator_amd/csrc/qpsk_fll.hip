@@ -113,6 +113,7 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
     static_assert(N == 40, "systolic FLL assumes 5 blocks of 8 taps");
     __shared__ FllSysLds L;
     if (a.kt && threadIdx.x == 0) kt_start(a.kt);
+    ClkSample clk{threadIdx.x == 0 ? a.clk : nullptr};
     if (threadIdx.x < 2 * N) L.taps[threadIdx.x] = P.lower_rev[threadIdx.x];
 
     const int lane = threadIdx.x & 63;

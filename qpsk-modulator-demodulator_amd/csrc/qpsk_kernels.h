@@ -18,6 +18,21 @@ constexpr int kModeConstellation = 1;
 // neighbours run on; recorded with vector atomics by a few lanes per launch.
 __device__ __forceinline__ void kt_start(unsigned long long *kt) { atomicMin(kt, wall_clock64()); }
 __device__ __forceinline__ void kt_end(unsigned long long *kt) { atomicMax(kt + 1, wall_clock64()); }
+// Clock sample (timed calls): one thread's lifetime in shader-clock ticks
+// (s_memtime) and wall ticks, added to clk[0], clk[1] when it goes out of
+// scope; the ratio is the clock the kernel ran at (qpsk_demod_kernel_clocks)
+struct ClkSample {
+    unsigned long long *clk, c0, r0;
+    __device__ explicit ClkSample(unsigned long long *p)
+        : clk(p), c0(p ? __builtin_amdgcn_s_memtime() : 0), r0(p ? wall_clock64() : 0) {}
+    __device__ ~ClkSample() {
+        if (clk) {
+            const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = wall_clock64();
+            atomicAdd(clk, c1 - c0);
+            atomicAdd(clk + 1, r1 - r0);
+        }
+    }
+};
 // records kt_end when it goes out of scope (every return path), lane 0 of each wave
 struct KtEnd {
     unsigned long long *kt;
@@ -66,6 +81,7 @@ struct LoopArgs {
     // starts, so the next pipelined call's FIR can wait until the loop kernel
     // holds its CUs (qpsk_runtime.hip, process_async_one)
     unsigned long long *resident;
+    unsigned long long *clk;   // clock sample of the M&M wave (ClkSample) or nullptr
 };
 
 // One internal chunk's rows appended behind what earlier chunks of the same
@@ -99,6 +115,7 @@ struct FllArgs {
     StreamState *state;
     int S;
     unsigned long long *kt;   // launch timestamps or nullptr
+    unsigned long long *clk;   // clock sample of each workgroup's first wave (ClkSample) or nullptr
 };
 
 struct IqbArgs {

@@ -185,6 +185,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     // the stage waves record the launch end as they leave (not the loader, whose
     // vmcnt waits count its own outstanding memory operations)
     KtEnd kte{wave != 0 ? a.kt : nullptr};
+    ClkSample clk{wave == 1 && lane == 0 ? a.clk : nullptr};
     // the batch spread evenly over the grid: workgroup b owns streams
     // [b S / G, (b + 1) S / G), at most SPW.  A workgroup left with few
     // streams (e.g. 16 of 24 at S = 256) runs its uniform loops ~10-25 %

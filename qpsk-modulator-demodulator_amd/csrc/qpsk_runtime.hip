@@ -75,7 +75,7 @@ int dev_alloc(T **p, size_t count) {
 
 // launch-timestamp slots per timed call: FLL, FIR, loop kernel (start, end)
 // and one spare pair; qpsk_demod_enable_timing records the first kKtCalls calls
-constexpr int kKtPerCall = 8;
+constexpr int kKtPerCall = 12;   // spans: FLL 0-1, FIR 2-3, loop 4-5; clock sums: FIR 6-7, FLL 8-9, loop 10-11
 constexpr int kKtCalls = 4096;
 constexpr int64_t kMaxSamplesPerCall = int64_t(1) << 30;
 // the symbol loop keeps sample indices of one call in 32-bit integers
@@ -294,6 +294,7 @@ void run_fll(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_l
     fa.lengths = d_len; fa.n = n_call;
     fa.state = h->d_state; fa.S = h->S;
     fa.kt = kt ? kt + 0 : nullptr;
+    fa.clk = kt ? kt + 8 : nullptr;
     launch_fll(fa, h->fp, st);
 }
 
@@ -366,6 +367,7 @@ int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipS
     la.flags = h->d_flags + (c.mem == QPSK_MEM_HOST ? 1 : 0);
     la.chunked = c.append ? 1 : 0;
     la.kt = kt ? kt + 4 : nullptr;
+    la.clk = kt ? kt + 10 : nullptr;
     la.resident = resident;
     const int grid = launch_loop(la, h->lp, c.mode, h->loop_variant, st);
     HIP_TRY(hipGetLastError());
@@ -706,7 +708,7 @@ int qpsk_demod_enable_timing(qpsk_demod *h, int32_t on) {
     const size_t n = static_cast<size_t>(kKtCalls) * kKtPerCall;
     if (!h->d_kt && (rc = dev_alloc(&h->d_kt, n))) return rc;
     // (start, end) pairs of slots 0-5: start = +inf for the atomic minimum, end
-    // = 0 for the maximum; slots 6-7 (FIR clock sums) = 0
+    // = 0 for the maximum; slots 6-11 (clock sums) = 0
     std::vector<unsigned long long> init(n, 0ull);
     for (size_t i = 0; i < n; i += 2)
         if (i % kKtPerCall < 6) init[i] = ~0ull;
@@ -764,7 +766,7 @@ int qpsk_demod_stage_times(qpsk_demod *h, float *ms, int32_t n) {
     return k;
 }
 
-int qpsk_demod_fir_clocks(qpsk_demod *h, float *ghz, int32_t max_calls) {
+int qpsk_demod_kernel_clocks(qpsk_demod *h, float *ghz, int32_t max_calls) {
     if (!h || !ghz) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
     if (!h->kt_used) return 0;
     int rc;
@@ -778,7 +780,12 @@ int qpsk_demod_fir_clocks(qpsk_demod *h, float *ghz, int32_t max_calls) {
     const int k = std::min<int32_t>(max_calls, h->kt_used);
     for (int c = 0; c < k; ++c) {
         const unsigned long long *s = t.data() + static_cast<size_t>(kKtPerCall) * c;
-        ghz[c] = s[7] ? static_cast<float>(static_cast<double>(s[6]) / s[7] * h->wall_khz * 1e-6) : 0.f;
+        // FLL (slots 8, 9), FIR (6, 7), loop kernel (10, 11)
+        const int slot[3] = {8, 6, 10};
+        for (int j = 0; j < 3; ++j) {
+            const unsigned long long cy = s[slot[j]], wt = s[slot[j] + 1];
+            ghz[3 * c + j] = wt ? static_cast<float>(static_cast<double>(cy) / wt * h->wall_khz * 1e-6) : 0.f;
+        }
     }
     return k;
 }

@@ -171,7 +171,7 @@ def lib():
     L.qpsk_demod_enable_timing.argtypes = [C.c_void_p, C.c_int32]
     L.qpsk_demod_stage_times.argtypes = [C.c_void_p, _f32p, C.c_int32]
     L.qpsk_demod_launch_times.argtypes = [C.c_void_p, _f32p, C.c_int32]
-    L.qpsk_demod_fir_clocks.argtypes = [C.c_void_p, _f32p, C.c_int32]
+    L.qpsk_demod_kernel_clocks.argtypes = [C.c_void_p, _f32p, C.c_int32]
     L.qpsk_demod_rrc_taps.argtypes = [C.c_void_p, _f32p, C.c_int32]
     L.qpsk_demod_gains.argtypes = [C.c_void_p] + [_f64p] * 5
     L.qpsk_demod_fll_taps.argtypes = [C.c_void_p, _f32p, _f32p, C.c_int32]
@@ -213,7 +213,7 @@ EXPORTED_SYMBOLS = [
     "qpsk_abi_version", "qpsk_last_error", "qpsk_demod_params_init", "qpsk_demod_create",
     "qpsk_demod_destroy", "qpsk_demod_set_stream", "qpsk_demod_process", "qpsk_demod_max_symbols",
     "qpsk_tsc_find", "qpsk_demod_enable_timing", "qpsk_demod_stage_times", "qpsk_demod_launch_times",
-    "qpsk_demod_fir_clocks",
+    "qpsk_demod_kernel_clocks",
     "qpsk_demod_rrc_taps",
     "qpsk_demod_gains", "qpsk_demod_fll_taps", "qpsk_demod_state_bytes", "qpsk_demod_get_state",
     "qpsk_demod_set_state", "qpsk_demod_design", "qpsk_framer_create", "qpsk_framer_destroy",
@@ -334,11 +334,12 @@ class BatchDemodulator:
         k = _check(lib().qpsk_demod_launch_times(self._h, out.ctypes.data_as(_f32p), max_calls))
         return out[:k].copy()
 
-    def fir_clocks(self, max_calls=4096) -> np.ndarray:
-        """[calls] float32: the shader clock (GHz) each recorded call's FIR ran
-        at (qpsk_demod_fir_clocks; 0 = no sample)."""
-        out = np.zeros(max_calls, dtype=np.float32)
-        k = _check(lib().qpsk_demod_fir_clocks(self._h, out.ctypes.data_as(_f32p), max_calls))
+    def kernel_clocks(self, max_calls=4096) -> np.ndarray:
+        """[calls, 3] float32: the shader clock (GHz) the FLL, FIR and loop
+        kernel of each recorded call ran at (qpsk_demod_kernel_clocks; 0 = the
+        kernel did not run)."""
+        out = np.zeros((max_calls, 3), dtype=np.float32)
+        k = _check(lib().qpsk_demod_kernel_clocks(self._h, out.ctypes.data_as(_f32p), max_calls))
         return out[:k].copy()
 
     def rrc_taps(self):

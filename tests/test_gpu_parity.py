@@ -346,16 +346,19 @@ def async_run(iq2d, calls, sps, span, sync_every=0, layout=None, **kw):
 
 
 @pytest.mark.parametrize("layout", ["direct", "staged"])
-@pytest.mark.parametrize("sync_every", [0, 2])
-def test_device_output_rows_in_place_or_staged(layout, sync_every):
+@pytest.mark.parametrize("sync_every,fll", [(0, False), (2, False), (0, True)])
+def test_device_output_rows_in_place_or_staged(layout, sync_every, fll):
     """Device calls whose rows the loop kernel can address are written in
     place (no 2-D copy behind it); misaligned or odd-stride rows go through
-    the staging buffers.  Both, synchronous and pipelined, equal the oracle."""
-    iq = K.batch_signals(4, seed0=470, sps=8, span=8, n_bits=2400, snr_db=16)
+    the staging buffers.  Both, synchronous and pipelined (with the FLL: the
+    loop kernel issued by the next call), equal the oracle."""
+    kw = dict(enable_fll=True, cfo_loop_bandwidth=1e-3) if fll else {}
+    okw = dict(enable_fll=True, cfo_loop_bw=1e-3) if fll else {}
+    iq = K.batch_signals(4, seed0=470, sps=8, span=8, n_bits=2400, snr_db=16, cfo_hz=2000.0 if fll else 0.0)
     n = iq.shape[1] // 2
     calls = [[n // 4] * 4, [n // 3] * 4, [n // 5] * 4, [n - n // 4 - n // 3 - n // 5] * 4]
-    got, _ = async_run(iq, calls, 8, 8, sync_every=sync_every, layout=layout)
-    assert_same(got, oracle_run(iq, calls, 8, 8))
+    got, _ = async_run(iq, calls, 8, 8, sync_every=sync_every, layout=layout, **kw)
+    assert_same(got, oracle_run(iq, calls, 8, 8, **okw))
 
 
 @pytest.mark.parametrize("fll", [False, True])
