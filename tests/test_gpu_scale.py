@@ -310,3 +310,43 @@ def test_chunked_host_call_reports_nonfinite():
     for s in range(S):
         assert Q.unpack_bits(bits[s], int(nb[s])) == K.oracle_for(8, 8).DeModulate(clean[s])
     b.close()
+
+
+@pytest.mark.parametrize("fll", [False, True])
+def test_launch_times_and_kernel_clocks(fll):
+    """enable_timing: every timed call records its kernels' own spans and
+    clock samples (qpsk_demod_launch_times / kernel_clocks), pipelined calls
+    included; the FLL column is empty with the FLL off; enable_timing restarts
+    the record; results do not change with timing on."""
+    import torch
+    S, n = 64, 1 << 15
+    iq = torch.from_numpy(K.batch_signals(S, seed0=1300, sps=8, span=8, n_bits=2 * n // 8 + 64,
+                                          snr_db=18)[:, : 2 * n].copy()).cuda()
+    kw = dict(enable_fll=True, cfo_loop_bandwidth=1e-3) if fll else {}
+    b = Q.BatchDemodulator(S, Q.params(K.FS, K.FS // 8, K.ALPHA, 8, max_samples_per_call=n, **kw))
+    ms = b.max_symbols(n)
+    bits = torch.zeros((S, ((2 * ms + 7) // 8 + 63) // 64 * 64), dtype=torch.uint8, device="cuda")
+    nb = torch.zeros(S, dtype=torch.int64, device="cuda")
+    b.process_device_async(iq, n, bits, nb)      # untimed
+    b.enable_timing(True)
+    for _ in range(3):
+        b.process_device_async(iq, n, bits, nb)
+    b.pipeline_wait()
+    lt, kc, st = b.launch_times(), b.kernel_clocks(), b.stage_times()
+    assert lt.shape == (3, 4) and kc.shape == (3, 3)
+    assert (lt[:, 1] > 0).all() and (lt[:, 2] > 0).all()
+    assert ((lt[:, 0] > 0) == fll).all()
+    assert (lt[:, 3] >= lt[:, :3].max(axis=1) * 0.999).all()
+    for j, ran in ((0, fll), (1, True), (2, True)):
+        if ran:
+            assert ((kc[:, j] > 0.3) & (kc[:, j] < 3.5)).all(), kc
+        else:
+            assert (kc[:, j] == 0).all()
+    assert abs(st["fir"] - lt[:, 1].mean()) < 1e-3 and abs(st["loop"] - lt[:, 2].mean()) < 1e-3
+    b.enable_timing(True)
+    assert b.launch_times().shape == (0, 4)
+    b.process_device_async(iq, n, bits, nb)
+    b.pipeline_wait()
+    assert b.launch_times().shape == (1, 4)
+    b.enable_timing(False)
+    b.close()
