@@ -536,3 +536,43 @@ def test_c_abi_demo_from_plain_c():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "bits identical to the oracle" in r.stdout
+
+
+@pytest.mark.parametrize("layout", ["direct", "staged"])
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_device_constellation_rows_in_place_or_staged(layout, pipelined):
+    """deModulateConstellation (QPSKDeModulator.cs:427-455) on device rows:
+    symbols written in place or through the staging copy, interleaved with
+    DeModulate calls on the same state, synchronous and pipelined."""
+    import torch
+    S = 4
+    iq = K.batch_signals(S, seed0=480, sps=8, span=8, n_bits=2400, snr_db=16)
+    n = iq.shape[1] // 2
+    calls = [[n // 3] * S, [n // 3] * S, [n - 2 * (n // 3)] * S]
+    modes = [Q.MODE_CONSTELLATION, Q.MODE_DEMODULATE, Q.MODE_CONSTELLATION]
+    b = Q.BatchDemodulator(S, Q.params(K.FS, K.FS // 8, K.ALPHA, 8, max_samples_per_call=n))
+    stream = torch.cuda.Stream()
+    b.set_stream(stream.cuda_stream)
+    ms = b.max_symbols(n)
+    outs, pos = [], 0
+    with torch.cuda.stream(stream):
+        for lens, m in zip(calls, modes):
+            k = lens[0]
+            xd = torch.from_numpy(np.ascontiguousarray(iq[:, 2 * pos: 2 * (pos + k)])).to("cuda")
+            bits, sy = out_rows(S, ms, layout)
+            nb = torch.zeros(S, dtype=torch.int64, device="cuda")
+            ns = torch.zeros(S, dtype=torch.int64, device="cuda")
+            f = b.process_device_async if pipelined else b.process_device
+            f(xd, k, bits if m == Q.MODE_DEMODULATE else None, nb if m == Q.MODE_DEMODULATE else None,
+              mode=m, syms_dev=sy, n_syms_dev=ns)
+            outs.append((xd, bits, nb, sy, ns, m))
+            pos += k
+    b.pipeline_wait()
+    torch.cuda.synchronize()
+    got = []
+    for _, bits, nb, sy, ns, m in outs:
+        bits, nb, sy, ns = bits.cpu().numpy(), nb.cpu().numpy(), sy.cpu().numpy(), ns.cpu().numpy()
+        got.append([(Q.unpack_bits(bits[s], int(nb[s])) if m == Q.MODE_DEMODULATE else "",
+                     sy[s, : 2 * int(ns[s])].copy()) for s in range(S)])
+    b.close()
+    assert_same(got, oracle_run(iq, calls, 8, 8, mode=modes))
