@@ -89,10 +89,11 @@ def reduce_stats(elapsed: float, counters, device=None):
     return float(t.item()), [int(v) for v in c.tolist()]
 
 
-def load_traffic(config_key: str):
-    """HBM bytes per FIR launch from the committed rocprofv3 PMC passes
-    (profiles/*pmc*.json, written by tools/pmc_traffic.py), or None."""
-    path = os.path.join(ROOT, "profiles", f"pmc_fir_{config_key}.json")
+def load_traffic(config_key: str, kernel: str = "fir"):
+    """HBM bytes per launch of one kernel (fir, loop, fll) from the committed
+    rocprofv3 PMC passes (profiles/pmc_<kernel>_<config>.json, written by
+    tools/pmc_traffic.py), or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{kernel}_{config_key}.json")
     try:
         with open(path) as f:
             return json.load(f).get("hbm_bytes_per_launch")
@@ -716,8 +717,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
                 "valu_frac_unfused": r.get("valu_frac_unfused"),
                 "clock_ghz": r.get("clock_ghz_median"),
                 "valu_frac_unfused_at_clock": r.get("valu_frac_unfused_at_clock"),
-                "traffic": (load_traffic(key) if dom == "fir" and S == cfg["streams"] and n == 1 << 20
-                            else None)}
+                "traffic": (load_traffic(key, dom) if S == cfg["streams"] and n == 1 << 20 else None)}
     rec = {
         "metric": METRIC,
         "value": round(value, 2),
