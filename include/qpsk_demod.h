@@ -27,7 +27,11 @@
 extern "C" {
 #endif
 
-#define QPSK_ABI_VERSION 1
+/* 2: versioned state blob (header + length checked by set_state; 256-sample
+ *    M&M carry), get_state / set_state take the buffer length and a non-const
+ *    handle (they flush pipelined work), qpsk_pipeline_gate_enabled.
+ * 1: rounds 1-3. */
+#define QPSK_ABI_VERSION 2
 
 /* status codes -> the C# exception each one replaces */
 #define QPSK_OK 0
@@ -151,11 +155,27 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
  *  - bits / n_bits / syms / n_syms are complete after qpsk_demod_pipeline_wait.
  *  - synchronous process(), get/set_state, set_stream and destroy first wait
  *    for every pipelined call.
+ *  - Residency gate: call k+1's matched filter waits ON THE DEVICE
+ *    (hipStreamWaitValue64, no timeout) until call k's symbol-loop workgroups
+ *    hold their CUs, so the two always overlap in the same order.  Under
+ *    serialised dispatch the loop kernel could only start after the waiting
+ *    filter, so the gate is off when qpsk_pipeline_gate_enabled() says so:
+ *    QPSK_PIPELINE_GATE=0, AMD_SERIALIZE_KERNEL or AMD_SERIALIZE_COPY != 0,
+ *    HIP_LAUNCH_BLOCKING or CUDA_LAUNCH_BLOCKING != 0, rocprofv3 counter
+ *    collection (ROCPROF_COUNTER_COLLECTION=1) or kernel serialisation
+ *    (ROCPROFILER_KERNEL_SERIALIZATION), HSA_ENABLE_DEBUG.  A tool that
+ *    serialises dispatch without any of these (e.g. a debugger attached after
+ *    start-up) can stall process_async: set QPSK_PIPELINE_GATE=0 for such runs
+ *    (results are identical with the gate off; only the overlap order may vary).
+ *    QPSK_PIPELINE_GATE=1 forces it on.  Read once per handle, at create.
  */
 int qpsk_demod_process_async(qpsk_demod *h, int32_t mode, const float *iq, int64_t stride_floats,
                              int64_t n_samples, const int64_t *lengths, uint8_t *bits,
                              int64_t bits_stride_bytes, int64_t *n_bits, float *syms,
                              int64_t syms_stride_floats, int64_t *n_syms);
+/* 1 if handles created now use the residency gate, 0 if the environment turns
+ * it off (the list above); needs no device. */
+int qpsk_pipeline_gate_enabled(void);
 /* OR of the QPSK_STATUS_* flags raised since the last qpsk_demod_status call
  * (waits for every queued call), then cleared.  0 = every call so far stayed
  * inside the reference's defined behaviour. */
@@ -218,10 +238,16 @@ int qpsk_demod_fll_taps(const qpsk_demod *h, float *lower_iq, float *upper_iq, i
 int qpsk_demod_design(const qpsk_demod_params *p, float *rrc_taps, int32_t cap, double *gains,
                       float *fll_lower_iq, float *fll_upper_iq);
 
-/* Loop state snapshot, one record per stream (checkpoint / chunk carry). */
+/* Loop state snapshot (checkpoint / migration): a 32-byte header (magic
+ * "QPSK", format 2, streams, RRC taps, carry length, FLL taps, record size)
+ * then one record per stream, the M&M carries, FIR histories and FLL delay
+ * lines.  get_state needs buf_bytes >= state_bytes; set_state needs exactly
+ * state_bytes and a header matching this handle, else QPSK_ERR_ARGUMENT (a
+ * blob of another handle shape or library version is never misread).  Both
+ * first wait for (and flush) pipelined calls. */
 int64_t qpsk_demod_state_bytes(const qpsk_demod *h);
-int qpsk_demod_get_state(const qpsk_demod *h, void *host_buf);
-int qpsk_demod_set_state(qpsk_demod *h, const void *host_buf);
+int qpsk_demod_get_state(qpsk_demod *h, void *host_buf, int64_t buf_bytes);
+int qpsk_demod_set_state(qpsk_demod *h, const void *host_buf, int64_t buf_bytes);
 
 /* ---------------------------------------------------------------------------
  * Host-fed streaming front-end: the deployment shape of

@@ -31,6 +31,24 @@
 //   a xi - b xr), exactly the reference's (hI*xI) - (hQ*xQ), (hI*xQ) + (hQ*xI)
 //   with hQ = -b (x - (-y) == x + y and x + (-y) == x - y in IEEE arithmetic).
 //
+//   The reference's FLL alpha is the constant 0 (Band-Edge Filter.cs:55), so
+//   `phase += freq + alpha * error` (:125) is `phase += freq` here: x + (+-0) == x
+//   for every x but +-0; freq just updated by `freq += beta * error` is -0 only
+//   if error < 0 (beta > 0; error is never -0), and then alpha * error is -0 too;
+//   only error = +-Inf differs (0 * Inf = NaN), and there the reference's NaN
+//   phase and this kernel's +-Inf phase, wrapped by IEEERemainder in the same
+//   step (:127, :185-189), are both NaN.  launch_fll sends a nonzero alpha to the
+//   one-lane kernel.
+//
+//   Main loop (blocks of 8 samples, 4 per iteration): the 32-sample window of
+//   mixed samples the partial sums read lives in registers, four 8-sample groups
+//   that rotate with the block position, and a block's outputs overwrite the
+//   oldest group in place (sample u of it is dead once step u starts).  The LDS
+//   ring serves only the first and the last blocks of a call.  The NCO's
+//   sinf/cosf is the lane-split form of qpsk_sincosf.h: the stream's even lanes
+//   run glibc's sin polynomial, its odd lanes the cos polynomial, one DPP swap
+//   hands each the other's value.
+//
 // Every float op is the reference's op in the reference's order
 // (-ffp-contract=off), so the output equals the one-lane fll_kernel bit for bit.
 #include <hip/hip_runtime.h>
@@ -87,14 +105,35 @@ __device__ __forceinline__ float dpp(float old, float v) {
 // lane i <- lane i-2 of its 16-lane row; row lanes 0, 1 (reference lane 0 of
 // both streams) read +0
 __device__ __forceinline__ float shr2(float v) { return dpp<0x112, 0xf, 0xf, true>(0.0f, v); }
-// every lane <- reference lane 7 of its stream (row lane 14 for even lanes, 15
-// for odd): quad_perm [2,3,2,3] fills quad 3 with the right values, row_ror:8
-// copies quad 3 to quad 1, and a 4-lane rotate (either direction lands on
-// quad 1 or 3) fills quads 0 and 2
-__device__ __forceinline__ float bcast7(float v) {
-    const float q = dpp<0xEE, 0xf, 0xf, false>(v, v);
-    const float r = dpp<0x128, 0xf, 0x2, false>(q, q);
-    return dpp<0x124, 0xf, 0x5, false>(r, r);
+// every lane <- reference lane 7 of its stream: row lane 14 (even lanes'
+// stream) or 15 (odd lanes'), row_newbcast:14 / :15 and a select on the lane's
+// parity (two independent DPP reads of v instead of a chain of three)
+__device__ __forceinline__ float bcast7(float v, bool odd) {
+    const int vi = __float_as_int(v);
+    const float e14 = __int_as_float(__builtin_amdgcn_mov_dpp(vi, 0x15E, 0xf, 0xf, false));
+    const float e15 = __int_as_float(__builtin_amdgcn_mov_dpp(vi, 0x15F, 0xf, 0xf, false));
+    return odd ? e15 : e14;
+}
+
+// sinf / cosf of y (|y| < 120 or NaN) by the lane-split form (qpsk_sincosf.h):
+// this lane's polynomial, its sign, a swap with the partner lane (l ^ 1 = row
+// lane +-2: quad_perm [2,3,0,1]) and the pick.  y must not be -0 unless ZFIX,
+// which keeps sin(-0) = -0 on the sin lanes (zy = 0 there, NaN on cos lanes).
+template <bool ZFIX>
+__device__ __forceinline__ void sincosf_split(float y, const qpsk_sincosf_lane &K, uint32_t signv, float zy,
+                                              float &sn, float &cs) {
+    uint32_t own, t;
+#define QPSK_FLL_SELECT(x, x2) (K.sin_lane ? (x) : (x2))
+    QPSK_SINCOSF_SPLIT_OWN(y, K, signv, QPSK_FLL_SELECT, own, t);
+#undef QPSK_FLL_SELECT
+    if constexpr (ZFIX) own = y == zy ? __float_as_uint(y) : own;
+    const uint32_t other = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(own), 0x4E, 0xf, 0xf, false));
+    uint32_t so, co, m;
+    asm("v_bfe_i32 %2, %3, 30, 1\n\tv_bfi_b32 %0, %2, %4, %5\n\tv_bfi_b32 %1, %2, %5, %4"
+        : "=&v"(so), "=&v"(co), "=&v"(m)
+        : "v"(t), "v"(own), "v"(other));
+    sn = __uint_as_float(so);
+    cs = __uint_as_float(co);
 }
 
 // Band-edge products of complex tap (a, b) [packed A = {a, a}, B = {b, b}] with
@@ -107,8 +146,19 @@ __device__ __forceinline__ void band_prod(f2 A, f2 B, f2 x, f2 &R, f2 &I) {
     R = add_xy_neghi(p, q);
     I = add_yx_neglo(p, q);
 }
+// the same with the tap as one register pair T = {a, b}: the broadcasts are
+// op_sel / op_sel_hi modifiers of the two v_pk_mul_f32 (half the tap VGPRs)
+__device__ __forceinline__ void band_prod(f2 T, f2 x, f2 &R, f2 &I) {
+    const f2 p = T.xx * x;   // {a xr, a xi}
+    const f2 q = T.yy * x;   // {b xr, b xi}
+    R = add_xy_neghi(p, q);
+    I = add_yx_neglo(p, q);
+}
 
-__global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
+// one wave per SIMD (C5: 1024 waves on 1024 SIMDs): the whole VGPR file is
+// this wave's, so the scheduler need not keep 256 free for a second one
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void fll_sys_kernel(FllArgs a, FllParams P) {
     constexpr int N = kFllTaps;
     static_assert(N == 40, "systolic FLL assumes 5 blocks of 8 taps");
     __shared__ FllSysLds L;
@@ -155,12 +205,13 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
     __syncthreads();
 
     // taps of this lane: reversed index l + 8j, as {a, a} and {b, b} pairs
-    f2 TA[5], TB[5];
+    f2 TA[5], TB[5], TT[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
         const float ta = L.taps[2 * (l + 8 * j)], tb = L.taps[2 * (l + 8 * j) + 1];
         TA[j] = f2{ta, ta};
         TB[j] = f2{tb, tb};
+        TT[j] = f2{ta, tb};
     }
 
     // pipeline state as after step -1: lane l (< 7) holds the lane sum over
@@ -212,7 +263,11 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
     // takes no literal): pinned once here, not rebuilt every sample
     uint32_t sign_v = 0x80000000u;
     asm volatile("" : "+v"(sign_v));
-    const float beta = P.beta, alpha = P.alpha, fmax_ = P.max_freq, fmin_ = P.min_freq;
+    const float beta = P.beta, fmax_ = P.max_freq, fmin_ = P.min_freq;
+    const bool odd = rl & 1;   // which stream of the DPP row (bcast7)
+    // lane-split sincos: even reference lanes evaluate the sin polynomial
+    const qpsk_sincosf_lane K = qpsk_sincosf_lane_init((l & 1) == 0);
+    const float zy = (l & 1) == 0 ? 0.0f : __builtin_nanf("");
 
     // one sample (Band-Edge Filter.cs:102-129) at t = t0 + u, t0 a multiple of 8.
     // FIRST: the call's first sample (the stored phase may be anything set_state
@@ -267,10 +322,10 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
 #if QPSK_FLL_PROBE & 4
         const float err = pw.y - pw.x;   // diagnostic: no broadcast
 #else
-        const float err = bcast7(pw.y - pw.x);
+        const float err = bcast7(pw.y - pw.x, odd);
 #endif
         freq = freq + beta * err;
-        phase = phase + (freq + alpha * err);
+        phase = phase + freq;   // alpha == 0 (file comment)
         if constexpr (decltype(exact)::value) {
             if (__builtin_expect(__ballot(fabsf(phase) > two_pi) != 0, 0))
                 if (fabsf(phase) > two_pi) phase = remainderf(phase, two_pi);
@@ -336,38 +391,131 @@ __global__ __launch_bounds__(256) void fll_sys_kernel(FllArgs a, FllParams P) {
         nmin = w2 < nmin ? w2 : nmin;
     }
     // Input: every lane of a stream loads the stream's 8 samples of a block
-    // (the same addresses for its 8 lanes).  Full double blocks run from two
-    // register buffers A and B, each reloaded right after its block, so a
-    // buffer's loads have a whole block to land and nothing is copied; the
-    // only vector-memory traffic between them is the previous block's y stores,
-    // and the wait before a block's first use covers just its own loads.
+    // (the same addresses for its 8 lanes).  Blocks run from two register
+    // buffers A and B, each reloaded right after its block, so a buffer's loads
+    // have a whole block to land.
     auto load8 = [&](f2 *buf, int64_t t0) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) buf[u] = x[t0 + u];
     };
-    int64_t t0 = 0;
-    if (nmin >= 16) {
-        f2 A[8], B[8];
-        load8(A, 0);
-        load8(B, 8);
-        if (nmin >= 32) {
-            block(A, 0, std::true_type{});
-            load8(A, 16);
-            block(B, 8, std::false_type{});
-            load8(B, 24);
-            for (t0 = 16; t0 + 32 <= nmin; t0 += 16) {
-                block(A, t0, std::false_type{});
-                load8(A, t0 + 16);
-                block(B, t0 + 8, std::false_type{});
-                load8(B, t0 + 24);
+
+    // ---- register-window blocks ------------------------------------------
+    // G[(p + i) & 3] holds x[t0 - 32 + 8i .. t0 - 25 + 8i] at block position p;
+    // step u overwrites G[p][u] with the block's output x[t0 + u].  The partial
+    // sums of steps 1..7 depend on the old window only (their newest input is
+    // x[t0 + u - 7]), so they are kept for a redo; step 8's (the next block's
+    // step 0) reads x[t0] = G[p][0], the block's first output.
+    f2 G[4][8];
+    bool need_exact = false;   // some lane's block-start phase is -0 (sincosf_split<false> excludes it)
+    auto rblock = [&](auto pc, const f2 *in, int64_t t0) __attribute__((always_inline)) {
+        constexpr int p = decltype(pc)::value;
+        auto X = [&](int k) __attribute__((always_inline)) -> f2 { return G[(p + (k >> 3)) & 3][k & 7]; };
+        const float ph0 = phase, fr0 = freq;
+        const f2 sr0 = SR, si0 = SI;
+        f2 QR[9], QI[9];
+        QR[0] = PR;
+        QI[0] = PI;
+        auto part = [&](int u) __attribute__((always_inline)) {   // QR/QI[u + 1]
+            f2 ar, ai;
+            band_prod(TT[0], X(u + 1), ar, ai);
+#pragma unroll
+            for (int j = 1; j < 4; ++j) {
+                f2 R, I;
+                band_prod(TT[j], X(u + 1 + 8 * j), R, I);
+                ar = ar + R;
+                ai = ai + I;
             }
-            block(A, t0, std::false_type{});
-            block(B, t0 + 8, std::false_type{});
-        } else {
-            block(A, 0, std::true_type{});
-            block(B, 8, std::false_type{});
+            QR[u + 1] = ar;
+            QI[u + 1] = ai;
+        };
+        float amax = 0.f, fmx = 0.f;
+        auto core = [&](f2 inu, int u, auto exact) __attribute__((always_inline)) {
+            float sn, cs;
+            sincosf_split<decltype(exact)::value>(phase, K, sign_v, zy, sn, cs);
+            const f2 xm = add_swap_neglo(inu * f2{cs, cs}, inu * f2{sn, sn});
+            G[p][u] = xm;
+            f2 R4, I4;
+            band_prod(TT[4], xm, R4, I4);
+            const f2 ar = QR[u] + R4, ai = QI[u] + I4;
+            SR = f2{shr2(SR.x) + ar.x, shr2(SR.y) + ar.y};
+            SI = f2{shr2(SI.x) + ai.x, shr2(SI.y) + ai.y};
+            const f2 pw = SR * SR + SI * SI;
+            const float err = bcast7(pw.y - pw.x, odd);
+            freq = freq + beta * err;
+            phase = phase + freq;   // alpha == 0 (file comment)
+            if constexpr (decltype(exact)::value) {
+                if (__builtin_expect(__ballot(fabsf(phase) > two_pi) != 0, 0))
+                    if (fabsf(phase) > two_pi) phase = remainderf(phase, two_pi);
+                freq = freq > fmax_ ? fmax_ : (freq < fmin_ ? fmin_ : freq);
+            } else {
+                amax = fmaxf(amax, fabsf(phase));   // NaN never wraps or clamps: ignored
+                fmx = fmaxf(fmx, fabsf(freq));
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            core(in[u], u, std::false_type{});
+            part(u);
         }
-        t0 += 16;
+        if (__builtin_expect((__ballot((amax > two_pi) | (fmx > fmax_)) != 0) | need_exact, 0)) {
+            // a wrap, a clamp or a -0 phase: redo the block exactly from its start
+            phase = ph0; freq = fr0; SR = sr0; SI = si0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) core(in[u], u, std::true_type{});
+            part(7);
+            // IEEERemainder can return -0 (an exact multiple of 2pi); a fast
+            // block never creates -0 (x + y == -0 needs x == -0)
+            need_exact = __ballot(__float_as_uint(phase) == 0x80000000u) != 0;
+        }
+        PR = QR[8];
+        PI = QI[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) y[t0 + u] = G[p][u];
+    };
+
+    int64_t t0 = 0;
+    if (nmin >= 56) {
+        {   // the call's first block (the full sinf/cosf on its first sample) from the ring
+            f2 cur[8];
+            load8(cur, 0);
+            block(cur, 0, std::true_type{});
+        }
+        t0 = 8;
+        // window x[t0-32 .. t0-1] from the ring: 16 aligned 16-B reads
+        const lds_f4 *wr = reinterpret_cast<const lds_f4 *>(ring + ((t0 - 32) & (kRingLen - 1)));
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const f4 v = wr[k];
+            G[k >> 2][(2 * k) & 7] = f2{v.x, v.y};
+            G[k >> 2][(2 * k + 1) & 7] = f2{v.z, v.w};
+        }
+        need_exact = __ballot(__float_as_uint(phase) == 0x80000000u) != 0;
+        f2 A[8], B[8];
+        load8(A, t0);
+        load8(B, t0 + 8);
+        do {
+            rblock(std::integral_constant<int, 0>{}, A, t0);
+            load8(A, t0 + 16);
+            rblock(std::integral_constant<int, 1>{}, B, t0 + 8);
+            load8(B, t0 + 24);
+            rblock(std::integral_constant<int, 2>{}, A, t0 + 16);
+            load8(A, t0 + 32);
+            rblock(std::integral_constant<int, 3>{}, B, t0 + 24);
+            load8(B, t0 + 40);
+            t0 += 32;
+        } while (t0 + 48 <= nmin);
+        // the window back into the ring (and its mirror) for the blocks that
+        // follow: group i at (t0 - 32 + 8i) & 63, a multiple of 8 samples
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            lds_f4 *ww = reinterpret_cast<lds_f4 *>(ring + ((t0 - 32 + 8 * i) & (kRingLen - 1)));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const f4 v = f4{G[i][2 * k].x, G[i][2 * k].y, G[i][2 * k + 1].x, G[i][2 * k + 1].y};
+                ww[k] = v;
+                ww[k + kRingLen / 2] = v;
+            }
+        }
     }
     // the rest (ragged streams, short calls, partly filled waves), block by block
     for (; t0 < nmax; t0 += 8) {

@@ -549,8 +549,9 @@ void launch_fir_hist(const FirArgs &a, float *hist_new, int H, int S, hipStream_
 
 void launch_fll(const FllArgs &a, const FllParams &P, hipStream_t stream) {
     // the systolic 8-lane kernel (qpsk_fll.hip) for the reference's Vector<float>
-    // width 8 and conjugate band-edge taps; the one-lane kernel otherwise
-    if (P.lanes == 8 && kFllTaps == 40 && P.conj_taps) {
+    // width 8, conjugate band-edge taps and alpha = 0 (Band-Edge Filter.cs:55,
+    // the only value the reference sets); the one-lane kernel otherwise
+    if (P.lanes == 8 && kFllTaps == 40 && P.conj_taps && P.alpha == 0.0f) {
         launch_fll_sys(a, P, stream);
         return;
     }

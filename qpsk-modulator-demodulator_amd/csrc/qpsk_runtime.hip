@@ -214,8 +214,7 @@ int flush_deferred(qpsk_demod *h);   // issues a deferred back stage (with the s
 
 // Host wait for every pipelined call issued so far (a deferred back stage is
 // issued first: every caller of this waits for all of the handle's work).
-int drain_async(const qpsk_demod *hc) {
-    qpsk_demod *h = const_cast<qpsk_demod *>(hc);
+int drain_async(qpsk_demod *h) {
     int rc;
     if ((rc = flush_deferred(h))) return rc;
     if (hipEvent_t e = last_async(h)) HIP_TRY(hipEventSynchronize(e));
@@ -591,11 +590,7 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
         h->wall_khz = 100000;
     if (h->loop_variant == 0 && h->lp.sps >= 8.0 && h->cus > 0 && (h->S + 23) / 24 <= h->cus / 2)
         h->loop_variant = 4;
-    {
-        const char *g = std::getenv("QPSK_PIPELINE_GATE");
-        const char *pmc = std::getenv("ROCPROF_COUNTER_COLLECTION");
-        h->use_gate = !((g && std::strcmp(g, "0") == 0) || (pmc && std::strcmp(pmc, "1") == 0));
-    }
+    h->use_gate = qpsk_pipeline_gate_enabled() == 1;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipStreamCreate failed"));
     h->own_stream = true;
@@ -1068,9 +1063,15 @@ int process_chunked(qpsk_demod *h, const Call &c, bool async) {
             // StreamState.tofs (the queue offset inside this call) non-zero,
             // which only the last chunk resets; clear it so the next call's
             // timing runs from its own queue start (best effort after a HIP error)
-            if (k > 0)
+            // The memset goes behind every kernel that may still write tofs:
+            // the pipelined chunks' loop kernels run on the back stream, and
+            // with the FLL the newest one is only issued by flush_deferred.
+            if (k > 0) {
+                (void)flush_deferred(h);
+                if (hipEvent_t e = last_async(h)) (void)hipStreamWaitEvent(h->stream, e, 0);
                 (void)hipMemset2DAsync(reinterpret_cast<char *>(h->d_state) + offsetof(StreamState, tofs),
                                        sizeof(StreamState), 0, sizeof(int64_t), S, h->stream);
+            }
             return rc;
         }
     }
@@ -1213,19 +1214,42 @@ int qpsk_demod_design(const qpsk_demod_params *p, float *rrc_taps, int32_t cap, 
     return T;
 }
 
+// State blob (format 2): a header naming the layout, then the per-stream
+// records, the M&M carries, the FIR histories and the FLL delay lines.  Format
+// 1 (round 3 and before) had no header and a 64-sample carry; set_state
+// rejects any blob whose header or length does not match this handle.
+namespace {
+constexpr uint32_t kStateMagic = 0x4b535051u;   // "QPSK"
+constexpr uint32_t kStateFormat = 2;
+struct StateHeader {
+    uint32_t magic, format;
+    int32_t streams, taps, carry_max, fll_taps, record_bytes, reserved;
+};
+static_assert(sizeof(StateHeader) == 32, "state blob header");
+StateHeader state_header(const qpsk_demod *h) {
+    return StateHeader{kStateMagic, kStateFormat, h->S, h->T, kCarryMax, kFllTaps,
+                       static_cast<int32_t>(sizeof(StreamState)), 0};
+}
+}  // namespace
+
 int64_t qpsk_demod_state_bytes(const qpsk_demod *h) {
     if (!h) return 0;
     const int64_t S = h->S, H = h->T - 1;
-    return S * (static_cast<int64_t>(sizeof(StreamState)) + 8 * kCarryMax + 8 * H + 8 * 2 * kFllTaps);
+    return static_cast<int64_t>(sizeof(StateHeader)) +
+           S * (static_cast<int64_t>(sizeof(StreamState)) + 8 * kCarryMax + 8 * H + 8 * 2 * kFllTaps);
 }
 
-int qpsk_demod_get_state(const qpsk_demod *h, void *host_buf) {
+int qpsk_demod_get_state(qpsk_demod *h, void *host_buf, int64_t buf_bytes) {
     if (!h || !host_buf) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    if (buf_bytes < qpsk_demod_state_bytes(h)) return fail(QPSK_ERR_ARGUMENT, "state buffer too small");
     const int64_t S = h->S, H = h->T - 1;
     char *p = static_cast<char *>(host_buf);
     int rc;
     if ((rc = drain_async(h))) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
+    const StateHeader hd = state_header(h);
+    std::memcpy(p, &hd, sizeof(hd));
+    p += sizeof(hd);
     HIP_TRY(hipMemcpy(p, h->d_state, S * sizeof(StreamState), hipMemcpyDeviceToHost));
     p += S * sizeof(StreamState);
     HIP_TRY(hipMemcpy(p, h->d_carry, S * 8 * kCarryMax, hipMemcpyDeviceToHost));
@@ -1236,10 +1260,25 @@ int qpsk_demod_get_state(const qpsk_demod *h, void *host_buf) {
     return QPSK_OK;
 }
 
-int qpsk_demod_set_state(qpsk_demod *h, const void *host_buf) {
+int qpsk_demod_set_state(qpsk_demod *h, const void *host_buf, int64_t buf_bytes) {
     if (!h || !host_buf) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    if (buf_bytes != qpsk_demod_state_bytes(h))
+        return fail(QPSK_ERR_ARGUMENT, "state blob length does not match this handle (" +
+                                           std::to_string(buf_bytes) + " vs " +
+                                           std::to_string(qpsk_demod_state_bytes(h)) + " bytes)");
+    const StateHeader want = state_header(h);
+    StateHeader got;
+    std::memcpy(&got, host_buf, sizeof(got));
+    if (got.magic != want.magic || got.format != want.format)
+        return fail(QPSK_ERR_ARGUMENT, "not a state blob of this library version (format " +
+                                           std::to_string(got.format) + ", expected " +
+                                           std::to_string(want.format) + ")");
+    if (got.streams != want.streams || got.taps != want.taps || got.carry_max != want.carry_max ||
+        got.fll_taps != want.fll_taps || got.record_bytes != want.record_bytes)
+        return fail(QPSK_ERR_ARGUMENT, "state blob layout (streams, taps, carry, record size) does not "
+                                       "match this handle");
     const int64_t S = h->S, H = h->T - 1;
-    const char *p = static_cast<const char *>(host_buf);
+    const char *p = static_cast<const char *>(host_buf) + sizeof(StateHeader);
     int rc;
     if ((rc = drain_async(h))) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1251,6 +1290,34 @@ int qpsk_demod_set_state(qpsk_demod *h, const void *host_buf) {
     p += S * 8 * H;
     HIP_TRY(hipMemcpy(h->d_fll_delay, p, S * 8 * 2 * kFllTaps, hipMemcpyHostToDevice));
     return QPSK_OK;
+}
+
+// Residency gate default (process_async_one).  hipStreamWaitValue64 cannot
+// time out, so the gate is off wherever dispatch may be serialised and the
+// loop kernel it waits for would only start after the waiting FIR.
+int qpsk_pipeline_gate_enabled(void) {
+    auto env = [](const char *name) -> const char * {
+        const char *v = std::getenv(name);
+        return v && *v ? v : nullptr;
+    };
+    auto is = [&](const char *name, const char *val) {
+        const char *v = env(name);
+        return v && std::strcmp(v, val) == 0;
+    };
+    auto nonzero = [&](const char *name) {
+        const char *v = env(name);
+        return v && std::strcmp(v, "0") != 0;
+    };
+    if (is("QPSK_PIPELINE_GATE", "0")) return 0;             // explicit opt-out
+    if (is("QPSK_PIPELINE_GATE", "1")) return 1;             // explicit opt-in wins over the rest
+    if (nonzero("AMD_SERIALIZE_KERNEL")) return 0;           // HIP runtime: serialised kernel launches
+    if (nonzero("AMD_SERIALIZE_COPY")) return 0;             // ... and copies
+    if (nonzero("HIP_LAUNCH_BLOCKING")) return 0;            // every launch waits for the previous
+    if (nonzero("CUDA_LAUNCH_BLOCKING")) return 0;           // the alias HIP also honours
+    if (is("ROCPROF_COUNTER_COLLECTION", "1")) return 0;     // rocprofv3 --pmc: per-dispatch serialisation
+    if (nonzero("ROCPROFILER_KERNEL_SERIALIZATION")) return 0;
+    if (nonzero("HSA_ENABLE_DEBUG")) return 0;               // debugger-attached runs
+    return 1;
 }
 
 }  // extern "C"

@@ -186,4 +186,85 @@ QPSK_HDF static inline void qpsk_sincosf_glibc_fast(float y, float *s, float *c)
 {
     qpsk_sincosf_glibc_fast_k(y, s, c, 0x80000000u);
 }
+
+/* Lane-split form for |y| < 120 or NaN, y != -0 (the FLL's kept phases, which
+ * are never -0 there: qpsk_fll.hip).  Two lanes share one argument: the "sin
+ * lane" evaluates glibc's sin polynomial, the "cos lane" its cos polynomial,
+ * through ONE instruction sequence with per-lane coefficients, and each then
+ * takes the other's result (a DPP swap on the device).
+ *
+ *   sin lane: m = x,  u = fma(m, 1, -0) = x,            v = m*x2 = x3, w = x7,
+ *             fma(v, S0, u), fma(x2, S2, S1)             -> glibc's sp
+ *   cos lane: m = x2, u = fma(m, C0, 1) = c1,           v = m*x2 = x4, w = x6,
+ *             fma(v, C1, u), fma(x2, C3, C2)             -> glibc's cp
+ *
+ * The polynomial runs on the unsigned reduced x.  glibc's sign placement (on
+ * xs for the sine, on cp for the cosine) is the same bits after the rounding:
+ * each op of the odd polynomial maps -x to the exact negative of its result
+ * and round-to-nearest is sign-symmetric; x = 0 only for y = +-0, and +0 gives
+ * +0 either way.  Quadrant n: the sine value carries the sign of bit 1 of n + 1
+ * and goes to sin(y) when n is even, the cosine value the sign of bit 1 of n
+ * and goes to sin(y) when n is odd.  With t = (n + T) << 30 (T = 1 on sin
+ * lanes, 0 on cos lanes) bit 31 of t is the lane's sign and bit 30 says
+ * whether the lane's own value is sin(y) (1) or cos(y) (0).
+ * tools/check_glibc_sincosf.c checks both lanes' views on every input. */
+struct qpsk_sincosf_lane {
+    double q, r, k1, k2, k3;   /* per-lane coefficients */
+    uint32_t tsh;              /* T << 30 */
+    int sin_lane;
+};
+
+QPSK_HDF static inline struct qpsk_sincosf_lane qpsk_sincosf_lane_init(int sin_lane)
+{
+    struct qpsk_sincosf_lane k;
+    k.sin_lane = sin_lane;
+    k.q = sin_lane ? 1.0 : -0x1.ffffffd0c621cp-2;
+    k.r = sin_lane ? -0.0 : 1.0;
+    k.k1 = sin_lane ? -0x1.555545995a603p-3 : 0x1.55553e1068f19p-5;
+    k.k2 = sin_lane ? 0x1.1107605230bc4p-7 : -0x1.6c087e89a359dp-10;
+    k.k3 = sin_lane ? -0x1.994eb3774cf24p-13 : 0x1.99343027bf8c3p-16;
+    k.tsh = sin_lane ? 0x40000000u : 0u;
+    return k;
+}
+
+/* The lane's own value (sign applied) and t; m is the lane's polynomial
+ * argument, chosen by the caller's select (x on sin lanes, x2 on cos lanes) */
+#define QPSK_SINCOSF_SPLIT_OWN(y, K, SIGNV, M_SELECT, own, t)                             \
+    do {                                                                                  \
+        const double yd_ = (double)(y);                                                   \
+        const double r_ = yd_ * 0x1.45F306DC9C883p+23;                                    \
+        const int n_ = ((int32_t)r_ + 0x800000) >> 24;                                    \
+        const double x_ = fma(-(double)n_, 0x1.921FB54442D18p0, yd_);                    \
+        const double x2_ = x_ * x_;                                                       \
+        const double m_ = M_SELECT(x_, x2_);                                              \
+        const double u_ = fma(m_, (K).q, (K).r);                                          \
+        const double v_ = m_ * x2_;                                                       \
+        const double w_ = v_ * x2_;                                                       \
+        const double a_ = fma(v_, (K).k1, u_);                                            \
+        const double b_ = fma(x2_, (K).k3, (K).k2);                                       \
+        const double p_ = fma(w_, b_, a_);                                                \
+        (t) = ((uint32_t)n_ << 30) + (K).tsh;                                             \
+        (own) = qpsk_f32_bits((float)p_) ^ ((t) & (SIGNV));                               \
+    } while (0)
+
+#define QPSK_SINCOSF_HOST_SELECT(x, x2) (k.sin_lane ? (x) : (x2))
+QPSK_HDF static inline uint32_t qpsk_sincosf_split_own(float y, struct qpsk_sincosf_lane k, uint32_t *t)
+{
+    uint32_t own, tt;
+    QPSK_SINCOSF_SPLIT_OWN(y, k, 0x80000000u, QPSK_SINCOSF_HOST_SELECT, own, tt);
+    *t = tt;
+    return own;
+}
+#undef QPSK_SINCOSF_HOST_SELECT
+
+/* own = this lane's value, other = the partner lane's */
+QPSK_HDF static inline void qpsk_sincosf_split_pick(uint32_t own, uint32_t other, uint32_t t, float *s, float *c)
+{
+    const uint32_t m = 0u - ((t >> 30) & 1u);
+    union { uint32_t u; float f; } so, co;
+    so.u = (own & m) | (other & ~m);
+    co.u = (other & m) | (own & ~m);
+    *s = so.f;
+    *c = co.f;
+}
 #endif

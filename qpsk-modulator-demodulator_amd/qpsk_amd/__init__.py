@@ -177,8 +177,9 @@ def lib():
     L.qpsk_demod_fll_taps.argtypes = [C.c_void_p, _f32p, _f32p, C.c_int32]
     L.qpsk_demod_state_bytes.argtypes = [C.c_void_p]
     L.qpsk_demod_state_bytes.restype = C.c_int64
-    L.qpsk_demod_get_state.argtypes = [C.c_void_p, C.c_void_p]
-    L.qpsk_demod_set_state.argtypes = [C.c_void_p, C.c_void_p]
+    L.qpsk_demod_get_state.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+    L.qpsk_demod_set_state.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+    L.qpsk_pipeline_gate_enabled.restype = C.c_int
     L.qpsk_framer_create.argtypes = [C.c_int32, _u8p, C.c_int32, _u8p, C.c_int32, C.c_int64,
                                      C.POINTER(C.c_void_p)]
     L.qpsk_framer_destroy.argtypes = [C.c_void_p]
@@ -216,7 +217,7 @@ EXPORTED_SYMBOLS = [
     "qpsk_demod_kernel_clocks",
     "qpsk_demod_rrc_taps",
     "qpsk_demod_gains", "qpsk_demod_fll_taps", "qpsk_demod_state_bytes", "qpsk_demod_get_state",
-    "qpsk_demod_set_state", "qpsk_demod_design", "qpsk_framer_create", "qpsk_framer_destroy",
+    "qpsk_demod_set_state", "qpsk_pipeline_gate_enabled", "qpsk_demod_design", "qpsk_framer_create", "qpsk_framer_destroy",
     "qpsk_framer_set_markers", "qpsk_framer_push", "qpsk_framer_dev_create",
     "qpsk_framer_dev_destroy", "qpsk_framer_dev_set_stream", "qpsk_framer_dev_set_markers",
     "qpsk_framer_dev_push", "qpsk_framer_dev_status", "qpsk_tsc_find_device",
@@ -281,7 +282,11 @@ def pack_bits(bits: str) -> np.ndarray:
     return np.packbits(a)
 
 
-# StreamState (csrc/qpsk_state.h), the head of a qpsk_demod_get_state blob
+# a qpsk_demod_get_state blob: a 32-byte header (magic "QPSK", format 2,
+# streams, taps, carry, FLL taps, record size), then StreamState[S]
+# (csrc/qpsk_state.h), carries, FIR histories, FLL delay lines
+STATE_HEADER_BYTES = 32
+# StreamState (csrc/qpsk_state.h)
 STREAM_STATE_DTYPE = np.dtype([("mu", "f8"), ("integ", "f8"), ("theta", "f8"), ("freq", "f8"),
                                ("base", "i4"), ("has_prev", "i4"), ("psi", "f4"), ("psq", "f4"),
                                ("pdi", "f4"), ("pdq", "f4"), ("carry_n", "i4"), ("diff_have", "i4"),
@@ -374,18 +379,21 @@ class BatchDemodulator:
     def get_state(self) -> bytes:
         n = lib().qpsk_demod_state_bytes(self._h)
         buf = C.create_string_buffer(n)
-        _check(lib().qpsk_demod_get_state(self._h, buf))
+        _check(lib().qpsk_demod_get_state(self._h, buf, n))
         return buf.raw
 
     def stream_states(self, blob: bytes | None = None) -> np.ndarray:
         """The per-stream loop state records (StreamState, csrc/qpsk_state.h)
         at the head of a get_state() blob, as a structured array [S]."""
         blob = self.get_state() if blob is None else blob
-        return np.frombuffer(blob[: self.S * STREAM_STATE_DTYPE.itemsize], dtype=STREAM_STATE_DTYPE)
+        return np.frombuffer(blob[STATE_HEADER_BYTES: STATE_HEADER_BYTES + self.S * STREAM_STATE_DTYPE.itemsize],
+                             dtype=STREAM_STATE_DTYPE)
 
     def set_state(self, blob: bytes):
-        buf = C.create_string_buffer(blob, len(blob))
-        _check(lib().qpsk_demod_set_state(self._h, buf))
+        """Restore a get_state() blob of a handle of the same shape (streams,
+        taps); any other blob raises (QPSK_ERR_ARGUMENT)."""
+        buf = C.create_string_buffer(bytes(blob), len(blob))
+        _check(lib().qpsk_demod_set_state(self._h, buf, len(blob)))
 
     # ---- host path --------------------------------------------------------
     def process(self, iq: np.ndarray, mode=MODE_DEMODULATE, lengths=None, want_syms=False):

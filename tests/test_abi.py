@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.check_output(["nm", "-D", "--defined-only", Q.LIB_PATH]).decode()
     for n in names:
         assert re.search(r"\bT " + n + r"\b", out), n
-    assert L.qpsk_abi_version() == 1
+    assert L.qpsk_abi_version() == 2
 
 
 def test_library_has_gfx950_code_object():
@@ -202,3 +202,37 @@ def test_create_rejects_bad_knobs_before_touching_a_device(kw):
     args.update(kw)
     h = C.c_void_p()
     assert Q.lib().qpsk_demod_create(C.byref(Q.params(**args)), 4, C.byref(h)) == Q.QPSK_ERR_ARGUMENT
+
+
+GATE_ENV = ["QPSK_PIPELINE_GATE", "AMD_SERIALIZE_KERNEL", "AMD_SERIALIZE_COPY", "HIP_LAUNCH_BLOCKING",
+            "CUDA_LAUNCH_BLOCKING", "ROCPROF_COUNTER_COLLECTION", "ROCPROFILER_KERNEL_SERIALIZATION",
+            "HSA_ENABLE_DEBUG"]
+
+
+@pytest.mark.parametrize("env,want", [
+    ({}, 1),
+    ({"QPSK_PIPELINE_GATE": "0"}, 0),
+    ({"QPSK_PIPELINE_GATE": "1", "AMD_SERIALIZE_KERNEL": "3"}, 1),   # explicit opt-in wins
+    ({"AMD_SERIALIZE_KERNEL": "1"}, 0),
+    ({"AMD_SERIALIZE_KERNEL": "3"}, 0),
+    ({"AMD_SERIALIZE_KERNEL": "0"}, 1),
+    ({"AMD_SERIALIZE_COPY": "2"}, 0),
+    ({"HIP_LAUNCH_BLOCKING": "1"}, 0),
+    ({"HIP_LAUNCH_BLOCKING": "0"}, 1),
+    ({"CUDA_LAUNCH_BLOCKING": "1"}, 0),
+    ({"ROCPROF_COUNTER_COLLECTION": "1"}, 0),
+    ({"ROCPROF_COUNTER_COLLECTION": "0"}, 1),
+    ({"ROCPROFILER_KERNEL_SERIALIZATION": "1"}, 0),
+    ({"HSA_ENABLE_DEBUG": "1"}, 0),
+    ({"AMD_SERIALIZE_KERNEL": ""}, 1),   # set but empty = unset
+])
+def test_pipeline_gate_predicate(monkeypatch, env, want):
+    """The residency gate (qpsk_runtime.hip, process_async_one) parks the FIR's
+    stream on hipStreamWaitValue64 with no timeout, so it must be off wherever
+    dispatch is serialised (include/qpsk_demod.h, qpsk_pipeline_gate_enabled);
+    evaluated without a device."""
+    for k in GATE_ENV:
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    assert Q.lib().qpsk_pipeline_gate_enabled() == want

@@ -33,8 +33,6 @@ pytestmark = pytest.mark.gpu
 N = 1 << 20
 CALLS = 7
 SEED = 0x5159534B            # bench.py synth_kw
-STATE_REC = 112              # sizeof(StreamState), csrc/qpsk_state.h
-THETA_IDX = 2                # StreamState.theta as the 3rd double of a record
 
 CASES = {
     # key: streams, sps, rrc span, impaired channel + FLL, pipelined calls
@@ -99,7 +97,7 @@ def test_baseline_workload_seven_calls_vs_libm_oracle(key, trig):
             b.pipeline_wait()
     stream.synchronize()
     assert b.status() == 0
-    theta = np.frombuffer(b.get_state()[: S * STATE_REC], dtype=np.float64).reshape(S, -1)[:, THETA_IDX]
+    theta = b.stream_states()["theta"]
     idx = list(range(8)) + list(range(S - 8, S))
     idx += [int(i) for i in np.argsort(-np.abs(theta)) if int(i) not in idx][:4]
     host = _rows(iq, idx)

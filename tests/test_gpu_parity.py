@@ -219,6 +219,18 @@ def test_state_checkpoint_roundtrip():
     for s in range(2):
         assert Q.unpack_bits(ba[s], int(na[s])) == ref[0][s][0]
         assert Q.unpack_bits(bb[s], int(nb[s])) == ref[1][s][0]
+    # a blob is only accepted by a handle of its own shape and format
+    hd = np.frombuffer(blob[: Q.STATE_HEADER_BYTES], dtype=np.uint32)
+    assert hd[0] == 0x4B535051 and hd[1] == 2 and hd[2] == 2
+    for bad in (blob[:-8], blob + b"\0" * 8, b"\0" * 4 + blob[4:], blob[:4] + b"\1\0\0\0" + blob[8:]):
+        with pytest.raises(ValueError):   # QPSK_ERR_ARGUMENT
+            b.set_state(bad)
+    c = Q.BatchDemodulator(3, p)   # three streams: another layout
+    with pytest.raises(ValueError):
+        c.set_state(blob)
+    c.close()
+    a.close()
+    b.close()
 
 
 def test_mirror_test_at_data_level():

@@ -5,8 +5,8 @@
  * every float input (stride 1 = all 2^32 bit patterns):
  *   glibc sinf / cosf  vs  the oracle restatement or_sinf / or_cosf
  *   (oracle/or_sincos.h)  vs  the product's fused qpsk_sincosf_glibc
- *   (csrc/qpsk_sincosf.h; the _small and branch-free _fast forms too where
- *   |x| < 120)
+ *   (csrc/qpsk_sincosf.h; the _small and branch-free _fast forms and the
+ *   FLL's lane-split form, both lanes' views, too where |x| < 120)
  * bit for bit (any NaN equals any NaN).  Prints "<checked> checked, <n> differ".
  *   gcc -O2 -fopenmp -ffp-contract=off -mfma -Ioracle \
  *       -Iqpsk-modulator-demodulator_amd/csrc -o /tmp/chk tools/check_glibc_sincosf.c -lm
@@ -47,6 +47,15 @@ int main(int argc, char **argv)
             ok = same(gs, ps) && same(gc, pc);
             qpsk_sincosf_glibc_fast(x, &ps, &pc);
             ok = ok && same(gs, ps) && same(gc, pc);
+            if (u != 0x80000000u) {   /* the lane-split form (y != -0): both lanes' views */
+                uint32_t ts, tc;
+                const uint32_t os = qpsk_sincosf_split_own(x, qpsk_sincosf_lane_init(1), &ts);
+                const uint32_t oc = qpsk_sincosf_split_own(x, qpsk_sincosf_lane_init(0), &tc);
+                qpsk_sincosf_split_pick(os, oc, ts, &ps, &pc);
+                ok = ok && same(gs, ps) && same(gc, pc);
+                qpsk_sincosf_split_pick(oc, os, tc, &ps, &pc);
+                ok = ok && same(gs, ps) && same(gc, pc);
+            }
         }
         if (!ok) {
             if (bad < 4) printf("differ at %08x\n", u);
