@@ -406,6 +406,57 @@ def split_gather(synth, demod_shard, S, n, world, rank, dev, host_collectives):
     return rec, gathered
 
 
+def gather_outputs(bits, nbits, world, rank, dev, host_collectives):
+    """The output path of SURVEY.md §8e after a sharded call: rank 0 gathers
+    every rank's packed bit rows and bit counts (dist.gather: RCCL on device
+    tensors, or gloo on host copies).  Each rank also contributes a checksum
+    of its own rows (all_gather of 3 int64), and rank 0 checks the gathered
+    blocks against them.  Returns (record with gather time, max over ranks,
+    and gathered bytes; the gathered tensors on rank 0, else None)."""
+    import torch
+    import torch.distributed as dist
+    cdev = torch.device("cpu") if host_collectives else dev
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    def checksum(b, c):
+        # row bytes as int64 sums weighted by position (a swapped or shifted
+        # block changes it), plus the bit counts
+        w = torch.arange(1, b.shape[1] + 1, dtype=torch.int64, device=b.device)
+        return torch.stack([(b.to(torch.int64) * w).sum(), c.to(torch.int64).sum(),
+                            torch.tensor(b.shape[0], dtype=torch.int64, device=b.device)])
+
+    own = checksum(bits, nbits).to(cdev)
+    sums = [torch.empty_like(own) for _ in range(world)]
+    dist.all_gather(sums, own)
+    sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    b, c = bits.to(cdev), nbits.to(cdev)
+    gb = [torch.empty_like(b) for _ in range(world)] if rank == 0 else None
+    gc = [torch.empty_like(c) for _ in range(world)] if rank == 0 else None
+    dist.gather(b, gb, dst=0)
+    dist.gather(c, gc, dst=0)
+    sync()
+    t1 = time.perf_counter()
+    ok = 1
+    if rank == 0:
+        ok = int(all(torch.equal(checksum(gb[r], gc[r]), sums[r]) for r in range(world)))
+    tt = torch.tensor([t1 - t0], dtype=torch.float64, device=cdev)
+    okt = torch.tensor([ok], dtype=torch.int64, device=cdev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dist.broadcast(okt, src=0)
+    nbytes = world * (b.numel() * b.element_size() + c.numel() * c.element_size())
+    rec = {"gather_ms": round(float(tt.item()) * 1e3, 3),
+           "gathered_GiB": round(nbytes / (1 << 30), 4),
+           "rows": world * b.shape[0],
+           "gathered_rows_match_rank_checksums": bool(okt.item()),
+           "collective": "gloo (host copies)" if host_collectives else "RCCL gather (device tensors)"}
+    return rec, ((torch.cat(gb), torch.cat(gc)) if rank == 0 else None)
+
+
 TSC_BITS = "11001010011101100100100110101100" + "01110100111001011010001101101001"  # testAtDataLevel.cs:20-22
 
 
@@ -692,6 +743,12 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
                 if rank == 0:
                     rec["cpu_baseline"], rec["parity_vs_libm_oracle"] = cpu, par
         del syms, nsyms
+    if world > 1 and S * bits.shape[1] * world <= (8 << 30):
+        # the §8e output path: every rank's bit rows (the untimed call's, or
+        # the last timed call's with --timed-only) and counts to rank 0
+        og, gathered = gather_outputs(bits, nbits, world, rank, dev, host_collectives=not nccl)
+        del gathered
+        rec["output_gather"] = og
     t_max, (errs, total_bits, lost, slips, bad_bits, bad_syms, n_port, libm_bad, libm_streams,
             steady_bad, steady_n) = reduce_stats(
         elapsed, [errs, total_bits, lost, slips, bad_bits, bad_syms, n_port, libm_bad, libm_streams,
@@ -732,7 +789,9 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
         "dtype": "f32/f64",
         "data": "synthetic (GPU-generated differential QPSK, RRC, +-1ppm LO pair"
                 + (", +-5kHz CFO, 4-tap multipath, 20 dB Es/N0" if cfg["impaired"] else "") + ")",
-        "config": {"workload": cfg["name"], "streams_per_gpu": S, "samples_per_stream": n,
+        "config": {"workload": (cfg["name"] if S == cfg["streams"] else
+                                f"{cfg['name']} [run with {S} streams/GPU (--streams)]"),
+                   "streams_per_gpu": S, "samples_per_stream": n,
                    "sps": sps, "taps": span * sps + 1, "fll": cfg["fll"],
                    "parallelism": f"stream-shard x{world}",
                    "costas_trig": "glibc sin/cos (bit-exact)" if args.costas_trig else

@@ -25,6 +25,10 @@
  * degree-5 correction; do_sin switches to a Taylor form below 0.126.
  *
  * Compile with -ffp-contract=off (the fma calls are explicit).
+ *
+ * Licence: restates glibc's s_sin.c / branred.c (Copyright (C) 2001-2022 Free
+ * Software Foundation, Inc., IBM Accurate Mathematical Library; LGPL-2.1-or-later)
+ * and carries that code's terms.  Test infrastructure only.
  */
 #ifndef OR_GLIBC_TRIG_H
 #define OR_GLIBC_TRIG_H

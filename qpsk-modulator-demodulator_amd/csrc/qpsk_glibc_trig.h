@@ -13,6 +13,12 @@
  * Host + device.  The sincos table is passed in (the loop kernel stages it in
  * LDS); toverp (Payne-Hanek, rare) is read from the constant copy.  Compile
  * with -ffp-contract=off (the fma calls are explicit).
+ *
+ * Licence: this restates the algorithm and constants of glibc's s_sin.c and
+ * branred.c (Copyright (C) 2001-2022 Free Software Foundation, Inc., IBM
+ * Accurate Mathematical Library), which are LGPL-2.1-or-later; this file and
+ * qpsk_glibc_tables.h carry that code's terms.  Pinned to glibc 2.35, x86-64
+ * FMA variant (tests/test_oracle.py GLIBC_PIN).
  */
 #ifndef QPSK_GLIBC_TRIG_H
 #define QPSK_GLIBC_TRIG_H

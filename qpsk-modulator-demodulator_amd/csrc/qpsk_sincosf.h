@@ -23,6 +23,12 @@
  * requires the product and oracle copies to agree.
  *
  * Host + device; compile with -ffp-contract=off (the fma calls are explicit).
+ *
+ * Licence: the algorithm and polynomial constants are those of glibc's
+ * sinf/cosf (contributed by Arm Ltd from its optimized-routines library,
+ * Copyright (c) 2018 Arm Ltd; LGPL-2.1-or-later in glibc, MIT OR Apache-2.0
+ * WITH LLVM-exception in optimized-routines).  Pinned to glibc 2.35
+ * (tests/test_oracle.py GLIBC_PIN).
  */
 #ifndef QPSK_SINCOSF_H
 #define QPSK_SINCOSF_H

@@ -197,3 +197,42 @@ def test_steady_state_check_replays_the_call_sequence():
     assert bench.steady_state_check(torch.from_numpy(iq), bits, nb, cfg, [0, 1, 2, 3], calls - 1)[0] > 0
     bits[2, 3] ^= 1
     assert bench.steady_state_check(torch.from_numpy(iq), bits, nb, cfg, [0, 1, 2, 3], calls) == (1, [2])
+
+
+# ---- the output gather of a sharded call, gloo ----
+def _og_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = bench.shard_streams(2 * SG_STREAMS, rank, world)
+        bits, nb = _sg_demod(_sg_synth(lo, hi - lo))
+        rec, gathered = bench.gather_outputs(bits, nb, world, rank, torch.device("cpu"), host_collectives=True)
+        q.put((rank, rec, None if gathered is None else (gathered[0].numpy(), gathered[1].numpy())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_output_gather_matches_single_process():
+    """bench.gather_outputs (the N > 1 sub-records' output path): rank 0 holds
+    every rank's rows in rank order, equal to one process demodulating the
+    whole batch, and the per-rank checksums agree."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_og_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted([q.get(timeout=180) for _ in range(2)], key=lambda t: t[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    rec0, (bits, nb) = res[0][1], res[0][2]
+    assert res[1][2] is None
+    for rec in (rec0, res[1][1]):
+        assert rec["gathered_rows_match_rank_checksums"] is True
+        assert rec["rows"] == 2 * SG_STREAMS and rec["gather_ms"] >= 0
+    rb, rnb = _sg_demod(_sg_synth(0, 2 * SG_STREAMS))
+    assert np.array_equal(nb, rnb.numpy())
+    assert bench.compare_rows(bits, nb, rb.numpy(), rnb.numpy())[0] == []

@@ -5,8 +5,9 @@ and C5 (8192 x 2^20, +-5 kHz CFO + multipath + AWGN, FLL on) run on the HIP
 path exactly as bench.py synthesises them (same generator, seeds and LO
 pair), through QPSKDeModulator.DeModulate semantics (QPSKDeModulator.cs:345-425):
 seven consecutive calls on the same buffer, as the bench's timed region
-feeds it.  Each call's bit rows of the first 8 and the last 8 streams (row
-offsets 32-64 GiB into the buffers), plus the 4 streams whose Costas phase
+feeds it.  Each call's bit rows of the first 8 and the last 8 streams (the
+last rows start 32 GiB into the input at C3 and the C4 shard and 64 GiB into
+it at C5; the assert below checks > 16 GiB for all three), plus the 4 streams whose Costas phase
 grew the most (QPSK false lock: |freq| near a multiple of pi/2, theta growing
 every symbol past the single +-2pi wrap of CostasLoopQpsk.cs:90-91, so the
 large-|theta| reduction paths run), are compared with the CPU oracle calling
@@ -71,7 +72,7 @@ def test_baseline_workload_seven_calls_vs_libm_oracle(key, trig):
                                lo_ppm=1.0, cfo_hz=5000.0 if imp else 0.0, multipath=imp,
                                esn0_db=20.0 if imp else None)
     del _tx
-    assert iq.stride(0) * 4 * (S - 1) > (16 << 30)   # last rows 32-64 GiB in
+    assert iq.stride(0) * 4 * (S - 1) > (16 << 30)   # last rows ~32 GiB (C3, C4) / ~64 GiB (C5) in
     b = Q.BatchDemodulator(S, Q.params(K.FS, K.FS // sps, K.ALPHA, span, enable_fll=imp,
                                        max_samples_per_call=N, costas_trig=trig))
     ms = b.max_symbols(N)
