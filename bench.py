@@ -714,7 +714,29 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
         steady_freq = [round(float(fr[i]), 4) for i in hot]
         steady_bad, steady_ex = steady_state_check(iq, bits, nbits, cfg, sidx, warmup + steps)
         steady_n = len(sidx)
+    fir_diag = None
     if not args.timed_only:
+        # untimed: where the FIR's cycles go beside the loop kernel (pipelined
+        # calls, as timed) and alone (serial calls: the FIR on an idle chip),
+        # per phase and by whether a loop workgroup shared the FIR's CU
+        # (qpsk_demod_enable_fir_phases), plus the FIR-alone launch time
+        fir_diag = {}
+        demod.enable_fir_phases(True)
+        demod.enable_timing(True)
+        for _ in range(4):
+            step()
+        drain()
+        torch.cuda.synchronize(dev)
+        fir_diag["phases_pipelined"] = demod.fir_phases()
+        demod.enable_timing(True)
+        for _ in range(4):
+            demod.process_device(iq, n, bits, nbits)
+        torch.cuda.synchronize(dev)
+        fir_diag["phases_alone"] = demod.fir_phases()
+        fir_diag["alone_rooflines"] = rooflines(demod.stage_times(), S, n, cfg, demod.launch_times(),
+                                                demod.kernel_clocks())
+        demod.enable_timing(False)
+        demod.enable_fir_phases(False)
         # untimed: one call from the initial state on every stream of the timed
         # handle (stream starts at t=0); its rows feed parity and BER
         syms = nsyms = None
@@ -765,7 +787,17 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
 
     value = world * S * n * steps / t_max / 1e6
     rl = rooflines(st, S, n, cfg, lt, kclk)
-    dom = max(rl, key=lambda k: rl[k]["ms"]) if rl else None
+    if fir_diag and "fir" in rl:
+        # the FIR alone (serial calls after the timed region; not `value`)
+        fa = fir_diag["alone_rooflines"].get("fir")
+        if fa:
+            rl["fir_alone"] = dict(fa, note="serial calls after the timed region: the FIR with the chip to "
+                                             "itself (untimed leg, not part of value)")
+        rl["fir"]["phases"] = {"pipelined": fir_diag["phases_pipelined"], "alone": fir_diag["phases_alone"],
+                               "unit": "shader cycles per sampled workgroup (every 64th), per phase",
+                               "note": "shared = a symbol-loop workgroup held the FIR workgroup's CU"}
+    timed = [k for k in rl if k != "fir_alone"]
+    dom = max(timed, key=lambda k: rl[k]["ms"]) if timed else None
     roof = None
     if dom:
         r = rl[dom]

@@ -225,6 +225,17 @@ int qpsk_demod_stage_times(qpsk_demod *h, float *ms, int32_t n);
 int qpsk_demod_launch_times(qpsk_demod *h, float *ms, int32_t max_calls);
 int qpsk_demod_kernel_clocks(qpsk_demod *h, float *ghz, int32_t max_calls);
 
+/* FIR phase sample (diagnostic): while on, every 64th matched-filter
+ * workgroup adds the shader cycles of its three phases -- stage (HBM -> LDS),
+ * products and sums, stores -- to one of two sums, chosen by whether a
+ * symbol-loop workgroup of this handle held its CU when it started (each loop
+ * workgroup marks its CU, read from the hardware HW_ID / XCC_ID registers).
+ * fir_phases: out[8 * shared + k], k = 0 stage, 1 compute, 2 store cycles, 3
+ * workgroups, shared = 0 free CU / 1 loop-shared CU (n >= 16); the sums are
+ * then cleared.  Returns 16. */
+int qpsk_demod_enable_fir_phases(qpsk_demod *h, int32_t on);
+int qpsk_demod_fir_phases(qpsk_demod *h, uint64_t *out, int32_t n);
+
 /* Design products, for parity checks against the reference constructor. */
 int qpsk_demod_rrc_taps(const qpsk_demod *h, float *taps, int32_t cap);
 int qpsk_demod_gains(const qpsk_demod *h, double *mm_sps, double *kp, double *ki,

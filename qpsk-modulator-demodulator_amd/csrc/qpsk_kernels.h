@@ -41,6 +41,20 @@ struct KtEnd {
     }
 };
 
+// The CU a wave runs on, as an index < kCuKeys: XCC_ID, then HW_ID's SE, SH
+// and CU fields (gfx9 layout: CU [11:8], SH [12], SE [15:13]).  Read from
+// hardware registers (s_getreg); diagnostic use (FIR phases).
+constexpr int kCuKeys = 2048;
+__device__ __forceinline__ unsigned cu_key() {
+    const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));     // hwreg(HW_REG_HW_ID)
+    const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));   // hwreg(HW_REG_XCC_ID)
+    return ((((xcc & 7u) * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u) + ((hw >> 8) & 15u);
+}
+// FIR phase sample (qpsk_demod_enable_fir_phases): phases[8 * shared + k],
+// k = 0 stage (HBM -> LDS), 1 products and sums, 2 stores, 3 workgroups;
+// shared = the loop kernel held the workgroup's CU when it started (cu_map)
+constexpr int kFirPhaseWords = 16;
+
 struct FirArgs {
     const float *x;        // [S][x_stride] float2 input
     int64_t x_stride;      // in float2
@@ -54,6 +68,10 @@ struct FirArgs {
     // or nullptr: {sum of shader-clock ticks, sum of wall ticks} over the
     // lifetimes of every kFirClockEvery-th workgroup (the clock the FIR runs at)
     unsigned long long *clk;
+    // or nullptr: per-phase shader cycles of every kFirClockEvery-th workgroup,
+    // split by whether a loop workgroup held its CU (cu_map, kCuKeys words)
+    unsigned long long *phases;
+    const unsigned *cu_map;
 };
 constexpr unsigned kFirClockEvery = 64;
 
@@ -82,6 +100,9 @@ struct LoopArgs {
     // holds its CUs (qpsk_runtime.hip, process_async_one)
     unsigned long long *resident;
     unsigned long long *clk;   // clock sample of the M&M wave (ClkSample) or nullptr
+    // or nullptr: cu_map[cu_key()] is 1 while a workgroup of this launch holds
+    // that CU (FIR phase sample, FirArgs.phases)
+    unsigned *cu_map;
 };
 
 // One internal chunk's rows appended behind what earlier chunks of the same

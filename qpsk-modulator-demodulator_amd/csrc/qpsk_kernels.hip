@@ -39,7 +39,10 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ int lds_slot(int i) { return i + ((i >> 6) << 3); }
 constexpr int lds_slots(int n) { return n + ((n >> 6) << 3) + 8; }
 
-constexpr int kFirThreads = 256;
+#ifndef QPSK_FIR_THREADS
+#define QPSK_FIR_THREADS 256   // A/B builds: 128 / 64 (1024- / 512-output tiles)
+#endif
+constexpr int kFirThreads = QPSK_FIR_THREADS;
 constexpr unsigned kKtLastWgs = 8192;
 
 // One output of the tile with the reference's full complex products
@@ -221,14 +224,26 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, const float *hr
     }
     const f2 *x = reinterpret_cast<const f2 *>(a.x) + s * a.x_stride;
     const f2 *hist = reinterpret_cast<const f2 *>(a.hist) + static_cast<int64_t>(s) * (T - 1);
+    // phase sample: shader-clock stamps at the phase boundaries (the barriers)
+    // and whether a loop workgroup holds this CU (glc read: the map entry was
+    // written through the XCD's L2 by the loop workgroup on this very CU)
+    const bool ph_wg = a.phases && tid == 0 && lin % kFirClockEvery == 0;
+    unsigned long long p0 = 0, p1 = 0, p2 = 0;
+    unsigned shared_cu = 0;
+    if (ph_wg) {
+        shared_cu = __hip_atomic_load(a.cu_map + cu_key(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        p0 = __builtin_amdgcn_s_memtime();
+    }
 
     fir_stage<T, NIN, VEC, NT>(lds, x, hist, tile0, n);
     __syncthreads();
+    if (ph_wg) p1 = __builtin_amdgcn_s_memtime();
 
     const int grp = tid / W, r = tid % W;
     f2 acc[Q];
     fir_core<T, W, Q>(lds + 72 * grp + r, r, hrev, acc);
     __syncthreads();
+    if (ph_wg) p2 = __builtin_amdgcn_s_memtime();
 #pragma unroll
     for (int q = 0; q < Q; ++q) lds[72 * grp + r + W * q] = acc[q];
     __syncthreads();
@@ -256,6 +271,14 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, const float *hr
             bad |= fir_nonfinite(v.x) | fir_nonfinite(v.y);
             if (g < n) y[g] = v;
         }
+    }
+    if (ph_wg) {
+        const unsigned long long p3 = __builtin_amdgcn_s_memtime();
+        unsigned long long *ph = a.phases + 8 * shared_cu;
+        atomicAdd(ph + 0, p1 - p0);
+        atomicAdd(ph + 1, p2 - p1);
+        atomicAdd(ph + 2, p3 - p2);
+        atomicAdd(ph + 3, 1ull);
     }
     if (__syncthreads_or(bad)) {
         const int o0 = 64 * (tid / W) + tid % W;

@@ -186,6 +186,16 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     // vmcnt waits count its own outstanding memory operations)
     KtEnd kte{wave != 0 ? a.kt : nullptr};
     ClkSample clk{wave == 1 && lane == 0 ? a.clk : nullptr};
+    // FIR phase sample: this workgroup's CU is marked while its M&M wave runs
+    struct CuMark {
+        unsigned *p;
+        __device__ explicit CuMark(unsigned *map) : p(map ? map + cu_key() : nullptr) {
+            if (p) __hip_atomic_store(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __device__ ~CuMark() {
+            if (p) __hip_atomic_store(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } cu_mark{wave == 1 && lane == 0 ? a.cu_map : nullptr};
     // the batch spread evenly over the grid: workgroup b owns streams
     // [b S / G, (b + 1) S / G), at most SPW.  A workgroup left with few
     // streams (e.g. 16 of 24 at S = 256) runs its uniform loops ~10-25 %

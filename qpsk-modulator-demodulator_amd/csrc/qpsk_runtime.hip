@@ -163,6 +163,11 @@ struct qpsk_demod {
     // written by the kernels themselves: qpsk_kernels.h kt_start / kt_end)
     unsigned long long *d_kt = nullptr;
     int kt_used = 0;
+    // FIR phase sample (qpsk_demod_enable_fir_phases): per-phase cycle sums
+    // [2][8] and the map of CUs a loop workgroup holds [kCuKeys]
+    bool fir_phases = false;
+    unsigned long long *d_phases = nullptr;
+    unsigned *d_cu_map = nullptr;
     int wall_khz = 100000;
     int cus = 0;
     // ---- pipelined calls (qpsk_demod_process_async) ----------------------
@@ -307,10 +312,15 @@ int run_fir(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_le
     fa.y = mf; fa.y_stride = h->mf_stride; fa.y_offset = kMfPrefix;
     fa.kt = kt ? kt + 2 : nullptr;
     fa.clk = kt ? kt + 6 : nullptr;
+    if (h->fir_phases) {
+        fa.phases = h->d_phases;
+        fa.cu_map = h->d_cu_map;
+    }
     if (n_call > 0) {
         launch_fir(fa, h->d_hrev, h->T, h->W, h->S, n_call, st);
         fa.kt = nullptr;
         fa.clk = nullptr;
+        fa.phases = nullptr;
         launch_fir_hist(fa, h->d_hist[h->hist_cur ^ 1], h->T - 1, h->S, st);
         h->hist_cur ^= 1;
     }
@@ -367,6 +377,7 @@ int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipS
     la.chunked = c.append ? 1 : 0;
     la.kt = kt ? kt + 4 : nullptr;
     la.clk = kt ? kt + 10 : nullptr;
+    la.cu_map = h->fir_phases ? h->d_cu_map : nullptr;
     la.resident = resident;
     const int grid = launch_loop(la, h->lp, c.mode, h->loop_variant, st);
     HIP_TRY(hipGetLastError());
@@ -655,6 +666,8 @@ int qpsk_demod_destroy(qpsk_demod *h) {
     }
     if (h->d_resident) hipFree(h->d_resident);
     hipFree(h->d_kt);
+    hipFree(h->d_phases);
+    hipFree(h->d_cu_map);
     hipFree(h->d_carry);
     hipFree(h->d_iqb);
     hipFree(h->d_state);
@@ -711,6 +724,37 @@ int qpsk_demod_enable_timing(qpsk_demod *h, int32_t on) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     HIP_TRY(hipMemcpy(h->d_kt, init.data(), n * sizeof(unsigned long long), hipMemcpyHostToDevice));
     return QPSK_OK;
+}
+
+int qpsk_demod_enable_fir_phases(qpsk_demod *h, int32_t on) {
+    if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
+    int rc;
+    if ((rc = drain_async(h))) return rc;
+    HIP_TRY(hipSetDevice(h->p.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (on && !h->d_phases) {
+        if ((rc = dev_alloc(&h->d_phases, kFirPhaseWords)) || (rc = dev_alloc(&h->d_cu_map, kCuKeys))) return rc;
+        HIP_TRY(hipMemset(h->d_cu_map, 0, kCuKeys * sizeof(unsigned)));
+    }
+    if (on) HIP_TRY(hipMemset(h->d_phases, 0, kFirPhaseWords * sizeof(unsigned long long)));
+    h->fir_phases = on != 0;
+    return QPSK_OK;
+}
+
+int qpsk_demod_fir_phases(qpsk_demod *h, uint64_t *out, int32_t n) {
+    if (!h || !out) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    if (n < kFirPhaseWords) return fail(QPSK_ERR_ARGUMENT, "n < 16");
+    if (!h->d_phases) {
+        std::memset(out, 0, kFirPhaseWords * sizeof(uint64_t));
+        return kFirPhaseWords;
+    }
+    int rc;
+    if ((rc = drain_async(h))) return rc;
+    HIP_TRY(hipSetDevice(h->p.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipMemcpy(out, h->d_phases, kFirPhaseWords * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(h->d_phases, 0, kFirPhaseWords * sizeof(unsigned long long)));
+    return kFirPhaseWords;
 }
 
 // per timed call: FLL, FIR and loop kernel durations and the call's kernel

@@ -180,6 +180,8 @@ def lib():
     L.qpsk_demod_get_state.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     L.qpsk_demod_set_state.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     L.qpsk_pipeline_gate_enabled.restype = C.c_int
+    L.qpsk_demod_enable_fir_phases.argtypes = [C.c_void_p, C.c_int32]
+    L.qpsk_demod_fir_phases.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     L.qpsk_framer_create.argtypes = [C.c_int32, _u8p, C.c_int32, _u8p, C.c_int32, C.c_int64,
                                      C.POINTER(C.c_void_p)]
     L.qpsk_framer_destroy.argtypes = [C.c_void_p]
@@ -217,7 +219,8 @@ EXPORTED_SYMBOLS = [
     "qpsk_demod_kernel_clocks",
     "qpsk_demod_rrc_taps",
     "qpsk_demod_gains", "qpsk_demod_fll_taps", "qpsk_demod_state_bytes", "qpsk_demod_get_state",
-    "qpsk_demod_set_state", "qpsk_pipeline_gate_enabled", "qpsk_demod_design", "qpsk_framer_create", "qpsk_framer_destroy",
+    "qpsk_demod_set_state", "qpsk_pipeline_gate_enabled", "qpsk_demod_enable_fir_phases",
+    "qpsk_demod_fir_phases", "qpsk_demod_design", "qpsk_framer_create", "qpsk_framer_destroy",
     "qpsk_framer_set_markers", "qpsk_framer_push", "qpsk_framer_dev_create",
     "qpsk_framer_dev_destroy", "qpsk_framer_dev_set_stream", "qpsk_framer_dev_set_markers",
     "qpsk_framer_dev_push", "qpsk_framer_dev_status", "qpsk_tsc_find_device",
@@ -324,6 +327,22 @@ class BatchDemodulator:
 
     def enable_timing(self, on=True):
         _check(lib().qpsk_demod_enable_timing(self._h, 1 if on else 0))
+
+    def enable_fir_phases(self, on=True):
+        _check(lib().qpsk_demod_enable_fir_phases(self._h, 1 if on else 0))
+
+    def fir_phases(self) -> dict:
+        """Mean shader cycles per sampled FIR workgroup and phase, on CUs a
+        loop workgroup held ("shared") and on the others ("free"); the sums
+        are cleared (qpsk_demod_fir_phases)."""
+        out = np.zeros(16, dtype=np.uint64)
+        _check(lib().qpsk_demod_fir_phases(self._h, out.ctypes.data, 16))
+        res = {}
+        for name, k in (("free", 0), ("shared", 1)):
+            cnt = int(out[8 * k + 3])
+            res[name] = {"workgroups": cnt, **{ph: (round(int(out[8 * k + i]) / cnt, 1) if cnt else None)
+                                               for i, ph in enumerate(("stage", "compute", "store"))}}
+        return res
 
     def stage_times(self):
         """Average kernel launch times (ms) of the calls since enable_timing:
