@@ -138,7 +138,7 @@ __device__ __forceinline__ void fir_core(const f2 *row, int r, const float *hrev
     if constexpr (J > 0 && W == 8) {
         // lane phase 0 unrolled, phases 1..7 as one rolled body: 6.8 KB of code
         // at T = 129 instead of 20.9 KB, and 2 % faster (C3 FIR alone 41.2 ->
-        // 40.4 ms, A/B x2, profiles/r02_fir_roll_ab.txt).  With l at run time,
+        // 40.4 ms, A/B x2, profiles/archive/r02_fir_roll_ab.txt).  With l at run time,
         // input l + 8i sits at row + l + 8i + 8(i/8), plus 8 more when
         // r + l + 8(i%8) >= 64, i.e. i%8 == 7 and r + l >= 8
         lane_phase(0, [&](int i) { return rd(W * i); });
@@ -530,7 +530,7 @@ static bool launch_fir_w8(const FirArgs &a, const float *hrev, int S,
     // workgroups beside the loop kernel's) measured the same at C3 and C2
     // (pipelined bench, A/B x2 on one MI355X), and so did a
     // work-sharing tile whose waves take 512-output units from an LDS counter
-    // (profiles/r02_fir_share_ab.txt)
+    // (profiles/archive/r02_fir_share_ab.txt)
     launch_fir_w8_nt<T, kFirThreads>(a, hrev, S, n_max, vec, stream);
     return true;
 }

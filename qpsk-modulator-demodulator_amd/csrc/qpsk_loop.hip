@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     // M&M and Costas chains too (on the copy of its samples the loader puts in
     // their ring rows) and write nothing.  A wave with 16 or fewer active lanes
     // runs these loops 10-50 % slower per symbol than one with 20 or more
-    // (profiles/r02_loop_probe_lanes.txt), so small batches keep SPW lanes busy
+    // (profiles/archive/r02_loop_probe_lanes.txt), so small batches keep SPW lanes busy
     const bool real = lane < nvalid;            // owns stream s: writes its results
     const bool valid = lane < SPW;              // computes stream sc
     const int sc = real ? s : blk_s0;
@@ -701,7 +701,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             // qpsk_sincos_arg); the fast pass assumes it does not and the round is
             // redone if it did.  Below 2^40 the fast pass is exact: a stream in a
             // QPSK false lock (|freq| > pi, theta growing every symbol) keeps the
-            // fast path for ~10^5 calls (profiles/r02_state_c3.log: a 4096-stream
+            // fast path for ~10^5 calls (profiles/archive/r02_state_c3.log: a 4096-stream
             // C3 batch has 27 such streams after 6 calls; with the old 1e6 range
             // their 26 workgroups redid every round and the kernel took 2.7x)
             auto widen = [](sym_t v) { return from_sym(v); };
@@ -916,7 +916,7 @@ int launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant, h
     hipLaunchKernelGGL(carry_prefix_kernel, dim3(a.S), dim3(64), 0, stream, a);
     // The loop is latency-bound per stream; a wave's lanes are free, so the
     // default (sps >= 2) is 32 streams x 64-sample rounds.  Measured at C2
-    // (profiles/r01_loop_probe.txt): 16 x 64 and 16 x 128 (half the barriers)
+    // (profiles/archive/r01_loop_probe.txt): 16 x 64 and 16 x 128 (half the barriers)
     // both run slower per symbol.  sps < 2 needs the 80-symbol round capacity,
     // which fits LDS at 16 streams x 64.  variant (qpsk_demod_params.loop_variant)
     // forces 1 = 16 x 64, 2 = 32 x 64, 3 = 16 x 128; all compute identical results.

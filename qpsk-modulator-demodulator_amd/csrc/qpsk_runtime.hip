@@ -593,7 +593,7 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
     // (256 workgroups) is the faster one (C5 serial loop 24.0 vs 39.2 ms).
     // Above half the CUs, too: no FIR workgroup fits beside a 147 KB one, and
     // pipelined calls then wait for the FIR (4096 streams: 37.7 vs 33.4 ms a
-    // call; 2048: 24.6 vs 29.1 ms, profiles/r02_loop_shapes_c4_ab.txt)
+    // call; 2048: 24.6 vs 29.1 ms, profiles/archive/r02_loop_shapes_c4_ab.txt)
     if (hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess)
         h->cus = 0;
     if (hipDeviceGetAttribute(&h->wall_khz, hipDeviceAttributeWallClockRate, p->device) != hipSuccess ||
@@ -975,7 +975,7 @@ int process_async_one(qpsk_demod *h, const Call &c) {
         // FIR finds no CU with room for its 104-147 KB workgroups and runs
         // after it (measured on MI355X at C3 under rocprofv3: FIR 42 + loop
         // 80 ms a call, against FIR 52 || loop 43 the other way round,
-        // profiles/r02_c3_dispatch_race.txt; reproduced by
+        // profiles/archive/r02_c3_dispatch_race.txt; reproduced by
         // tools/anyorder_probe.hip), and either order then repeats call after
         // call.  So FIR(k+1) waits, on the device, until loop(k)'s workgroups
         // hold their CUs: each adds 1 to the residency counter as it starts,
