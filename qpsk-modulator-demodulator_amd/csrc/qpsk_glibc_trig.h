@@ -457,6 +457,182 @@ QPSK_GHD static inline void qpsk_gl_split_finish(double x, const qpsk_gl_split_a
     *c_out = c;
 }
 
+/* ---- fast split form (round 4): both halves work on |x| ---------------------
+ * For |x| < QPSK_GLIBC_SMALL_LIMIT (or NaN) glibc's pair is odd/even in x bit
+ * for bit: sin(x) = sign(x) * sin(|x|), cos(x) = cos(|x|) -- every operation of
+ * do_sin, do_cos, TAYLOR_SIN and reduce_sincos maps -x (with -dx) to the exact
+ * negative (round-to-nearest is sign-symmetric, and TOINT + k rounds ties to
+ * the even k whatever its sign), so the region logic, the dx flips and the
+ * sign bookkeeping of the general form run once, on |x|:
+ *   |x| < 0.855469:  sin = do_sin(|x|, 0)      cos = do_cos(|x|, 0)
+ *   |x| < 2.426265:  sin = do_cos(y, hp1)      cos = do_sin(y + hp1, da)   (y = hp0 - |x|)
+ *   otherwise:       n, b, db = reduce_sincos(|x|); sin = do_sin(b, db) / do_cos(b, db)
+ *                    by n & 1, signs by bit 1 of n (sin) and of n + 1 (cos)
+ * and the sign of x goes onto the sine at the end.  glibc's |x| < 2^-26 (sin =
+ * x) and |x| < 2^-27 (cos = 1) shortcuts need no branch: TAYLOR_SIN and the
+ * table path round to exactly those values there.
+ * The two halves differ only by per-lane constants (qpsk_gl_fs_lane), so they
+ * run ONE instruction sequence: with L0 = 1, L1 = 0 (do_sin half) or L0 = 0,
+ * L1 = 1 (do_cos half)
+ *   xr = fma(d, L1, z)                    do_cos adds dx, do_sin does not
+ *   s  = fma(q, p, fma(xr, L1, d*L0)) + xr*L0
+ *                                         do_sin: xr + fma(q, p, d); do_cos: fma(q, p, xr)
+ *   c  = fma(xr, d*L0, X)                 do_sin: xr*d + X;  do_cos: X
+ * (a zero product adds a signed zero to a value that is never -0, so each is
+ * the op it replaces bit for bit), and B = y + hp1 * L0 is the do_sin half's
+ * y + hp1 and the do_cos half's y.  Each half's result carries the sign its
+ * value has in the pair (bit 1 of n + 1 on the do_sin half, of n on the do_cos
+ * half, region C only), so after the exchange only the swap (region B, or n
+ * odd) and the sign of x remain.  tools/check_glibc_sin.c -DWITH_PRODUCT checks
+ * the assembled pair against the real libm. */
+typedef struct {
+    double L0, L1, hp1L;    /* 1, 0, hp1 on the do_sin half; 0, 1, 0 on the do_cos half */
+    uint32_t sgnm;          /* 0x80000000 on the do_sin half (copysign), 0 on the other */
+    uint32_t tsh;           /* 1 << 30 on the do_sin half: its sign is bit 1 of n + 1 */
+    uint32_t sign;          /* 0x80000000 on both */
+    int sin_half;
+    /* the fma addends of the polynomials and the reduction (uniform): device
+     * code pins them in VGPRs, so no iteration rebuilds them from SGPR halves
+     * (a VOP3 op reads one scalar operand) */
+    double toint, s4, sn3, cs4;
+} qpsk_gl_fs_lane;
+
+QPSK_GHD static inline qpsk_gl_fs_lane qpsk_gl_fs_lane_init(int sin_half)
+{
+    qpsk_gl_fs_lane k;
+    k.L0 = sin_half ? 1.0 : 0.0;
+    k.L1 = sin_half ? 0.0 : 1.0;
+    k.hp1L = sin_half ? QPSK_GL_HP1 : 0.0;
+    k.sgnm = sin_half ? 0x80000000u : 0u;
+    k.tsh = sin_half ? 0x40000000u : 0u;
+    k.sign = 0x80000000u;
+    k.sin_half = sin_half;
+    k.toint = QPSK_GL_TOINT;
+    k.s4 = QPSK_GL_S4;
+    k.sn3 = QPSK_GL_SN3;
+    k.cs4 = QPSK_GL_CS4;
+    return k;
+}
+
+/* hi-word bit helpers: (m & a) | (~m & b), and (v << 5) + base */
+QPSK_GHD static inline uint32_t qpsk_gl_bfi(uint32_t m, uint32_t a, uint32_t b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+#else
+    return (m & a) | (~m & b);
+#endif
+}
+
+QPSK_GHD static inline double qpsk_gl_with_hi(double v, uint32_t hi)
+{
+    return qpsk_gl_from_bits((qpsk_gl_bits(v) & 0xffffffffull) | ((uint64_t)hi << 32));
+}
+
+QPSK_GHD static inline uint32_t qpsk_gl_hi(double v) { return (uint32_t)(qpsk_gl_bits(v) >> 32); }
+
+/* this half's argument of |x|; *t = n << 30 in region C (bit 31 = bit 1 of
+ * n, bit 30 = bit 0), 0 elsewhere; *swap: the do_cos half's value is sin(|x|)
+ * (region B, or region C with n odd) */
+QPSK_GHD static inline double qpsk_gl_fs_prepare(double x, const qpsk_gl_fs_lane *K, double *dxa, uint32_t *t,
+                                                 int *swap)
+{
+    const double ax = fabs(x);
+    /* region C: reduce_sincos(|x|) */
+    const double tt = fma(ax, QPSK_GL_HPINV, K->toint);
+    const double xn = tt - QPSK_GL_TOINT;
+    double y = fma(-xn, QPSK_GL_MP1, ax);
+    y = fma(-xn, QPSK_GL_MP2, y);
+    const double t2 = fma(-xn, QPSK_GL_PP3, y);
+    double db = fma(-xn, QPSK_GL_PP3, y - t2);
+    const double b = fma(-xn, QPSK_GL_PP4, t2);
+    db = db + fma(-xn, QPSK_GL_PP4, t2 - b);
+    /* region B */
+    const double yb = QPSK_GL_HP0 - ax;
+    const double xb = yb + K->hp1L;
+    const double dB = (yb - xb) + QPSK_GL_HP1;
+    const int rA = ax < 0x1.b6p-1;                   /* hi word < 0x3feb6000 */
+    const int rB = ax < 0x1.368fdp+1;                /* hi word < 0x400368fd */
+    *dxa = rA ? 0.0 : (rB ? dB : db);
+    const uint32_t tn = (uint32_t)qpsk_gl_bits(tt) << 30;
+    *t = rB ? 0u : tn;
+    *swap = rA ? 0 : (rB ? 1 : (int)(tn >> 30) & 1);
+    return rA ? ax : (rB ? xb : b);
+}
+
+/* do_sin (K->sin_half) or do_cos of (xa, dxa), with the sign it takes in the
+ * pair: t from qpsk_gl_fs_prepare */
+QPSK_GHD static inline double qpsk_gl_fs_half(double xa, double dxa, uint32_t t, const qpsk_gl_fs_lane *K,
+                                              const double *tabh)
+{
+    /* TAYLOR_SIN (qpsk_gl_taylor_sin) with the pinned addend */
+    const double ta = xa * xa;
+    double tp = fma(ta, QPSK_GL_S5, K->s4);
+    tp = fma(ta, tp, QPSK_GL_S3);
+    tp = fma(ta, tp, QPSK_GL_S2);
+    tp = fma(ta, tp, QPSK_GL_S1);
+    const double ty = xa + fma(ta, fma(tp, xa, -(0.5 * dxa)), dxa);
+    /* d = dx, negated when xa < 0 (xa is never -0): the sign of xa XORed in */
+    const double d = qpsk_gl_with_hi(dxa, qpsk_gl_hi(dxa) ^ (qpsk_gl_hi(xa) & K->sign));
+    const double ax = fabs(xa);
+    const double u = QPSK_GL_BIG + ax;
+    const double xr = fma(d, K->L1, ax - (u - QPSK_GL_BIG));
+    const double xx = xr * xr;
+    const double q = xr * xx;
+    const double p = fma(xx, QPSK_GL_SN5, K->sn3);
+    const double dl = d * K->L0;
+    const double s = fma(q, p, fma(xr, K->L1, dl)) + xr * K->L0;
+    const double c = fma(xr, dl, xx * fma(xx, fma(xx, QPSK_GL_CS6, K->cs4), QPSK_GL_CS2));
+    /* valid arguments give node <= 109; NaN any bits (stays in the table region) */
+    const uint32_t node = (uint32_t)qpsk_gl_bits(u) & 127u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    /* the table is in LDS: a 32-bit LDS address, node * 32 B + base in one op */
+    typedef __attribute__((address_space(3))) const double lds_double;
+    uint32_t addr;
+    asm("v_lshl_add_u32 %0, %1, 5, %2"
+        : "=v"(addr)
+        : "v"(node), "v"((uint32_t)(uintptr_t)(lds_double *)tabh));
+    lds_double *tb = (lds_double *)(uintptr_t)addr;
+#else
+    const double *tb = tabh + 4 * node;
+#endif
+    double cor = fma(s, tb[0], tb[1]);
+    cor = fma(-c, tb[2], cor);
+    cor = fma(s, tb[3], cor);
+    const double r = tb[2] + cor;
+    /* do_sin: copysign(r, xa) (r > 0); do_sin below 0.126: TAYLOR_SIN */
+    double v = qpsk_gl_with_hi(r, qpsk_gl_bfi(K->sgnm, qpsk_gl_hi(xa), qpsk_gl_hi(r)));
+    if (K->sin_half && ax < 0.126) v = ty;
+    /* the pair's sign of this value (region C) */
+    return qpsk_gl_with_hi(v, qpsk_gl_hi(v) ^ ((t + K->tsh) & K->sign));
+}
+
+/* sin and cos of x from the do_sin half's value VS and the do_cos half's VC */
+QPSK_GHD static inline void qpsk_gl_fs_finish(double x, int swap, double VS, double VC, const qpsk_gl_fs_lane *K,
+                                              double *s_out, double *c_out)
+{
+    const double s = swap ? VC : VS, c = swap ? VS : VC;
+    *s_out = qpsk_gl_with_hi(s, qpsk_gl_hi(s) ^ (qpsk_gl_hi(x) & K->sign));
+    *c_out = c;
+}
+
+/* host form of the fast split pair (both halves in one thread), for the checker */
+QPSK_GHD static inline void qpsk_glibc_sincos_fs_host(double x, const double *tabs, const double *tabc,
+                                                      double *s_out, double *c_out)
+{
+    const qpsk_gl_fs_lane k0 = qpsk_gl_fs_lane_init(1), k1 = qpsk_gl_fs_lane_init(0);
+    double d0, d1;
+    uint32_t t0, t1;
+    int w0, w1;
+    const double x0 = qpsk_gl_fs_prepare(x, &k0, &d0, &t0, &w0);
+    const double x1 = qpsk_gl_fs_prepare(x, &k1, &d1, &t1, &w1);
+    const double VS = qpsk_gl_fs_half(x0, d0, t0, &k0, tabs);
+    const double VC = qpsk_gl_fs_half(x1, d1, t1, &k1, tabc);
+    qpsk_gl_fs_finish(x, w0, VS, VC, &k0, s_out, c_out);
+}
+
 /* host form of the split evaluation (both halves in one thread), for the checker */
 QPSK_GHD static inline void qpsk_glibc_sincos_split_host(double x, const double *tabs, const double *tabc,
                                                          double *s_out, double *c_out)

@@ -664,6 +664,10 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         const int csc = TRIG ? __shfl(sc, cl, 64) : sc;
         const int half = TRIG ? (lane >> 5) : 0;
         const double *tabh = L.tab + (half ? 440 : 0);
+        // fast-split lane constants: the lower half runs do_sin, the upper do_cos
+        qpsk_gl_fs_lane KF = qpsk_gl_fs_lane_init(half == 0);
+        asm volatile("" : "+v"(KF.L0), "+v"(KF.L1), "+v"(KF.hp1L), "+v"(KF.sgnm), "+v"(KF.tsh), "+v"(KF.sign));
+        asm volatile("" : "+v"(KF.toint), "+v"(KF.s4), "+v"(KF.sn3), "+v"(KF.cs4));
         double theta = 0.0, freq = 0.0;
         if (cmine) {
             theta = a.state[csc].theta;
@@ -709,7 +713,17 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const d2 yn = widen(in[k + 1]);   // next symbol, read and widened under this one's chain
                 double sn, cs;
                 // Math.Sin/Cos = glibc; the fast pass leaves its Payne-Hanek reduction out
-                if constexpr (TRIG) {
+                if constexpr (TRIG && !decltype(huge)::value) {
+                    // the fast pass: the pair of |theta| (qpsk_glibc_trig.h, fast split form)
+                    double dxa;
+                    uint32_t tq;
+                    int sw;
+                    const double xa = qpsk_gl_fs_prepare(theta, &KF, &dxa, &tq, &sw);
+                    const double rh = qpsk_gl_fs_half(xa, dxa, tq, &KF, tabh);
+                    double VS, VC;
+                    swap_halves(rh, &VS, &VC);
+                    qpsk_gl_fs_finish(theta, sw, VS, VC, &KF, &sn, &cs);
+                } else if constexpr (TRIG) {
                     const qpsk_gl_split_arg g = qpsk_gl_split_prepare(theta, half, decltype(huge)::value);
                     const double rh = qpsk_gl_do_half(g.xa, g.dxa, half, tabh);
                     double DS, DC;

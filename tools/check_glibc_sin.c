@@ -70,6 +70,14 @@ static void check(double x)
         if (n_bad < 20) printf("x=%a split sin %a cos %a vs oracle %a %a\n", x, ss, sc, s, c);
         ++n_bad;
     }
+    if (!(fabs(x) >= QPSK_GLIBC_SMALL_LIMIT)) {   /* the fast split pair (its range, NaN included) */
+        double fs, fc;
+        qpsk_glibc_sincos_fs_host(x, g_tabs, g_tabc, &fs, &fc);
+        if (!same(fs, s) || !same(fc, c)) {
+            if (n_bad < 20) printf("x=%a fast split sin %a cos %a vs oracle %a %a\n", x, fs, fc, s, c);
+            ++n_bad;
+        }
+    }
 #endif
     if (!same(s, rs) || !same(c, rc)) {
         if (n_bad < 20)
