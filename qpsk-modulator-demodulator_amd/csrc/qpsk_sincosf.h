@@ -238,8 +238,11 @@ QPSK_HDF static inline struct qpsk_sincosf_lane qpsk_sincosf_lane_init(int sin_l
 #define QPSK_SINCOSF_SPLIT_OWN(y, K, SIGNV, M_SELECT, own, t)                             \
     do {                                                                                  \
         const double yd_ = (double)(y);                                                   \
-        const double r_ = yd_ * 0x1.45F306DC9C883p+23;                                    \
-        const int n_ = ((int32_t)r_ + 0x800000) >> 24;                                    \
+        /* glibc's ((int32_t)(yd * 2^24 * 2/pi) + 0x800000) >> 24 with the 2^23 folded   \
+         * into the product's rounding: the same n for every |y| < 120 (all 2^32 inputs \
+         * checked, tools/check_glibc_sincosf.c), one integer add fewer */              \
+        const double r_ = fma(yd_, 0x1.45F306DC9C883p+23, 0x1p23);                        \
+        const int n_ = (int32_t)r_ >> 24;                                                 \
         const double x_ = fma(-(double)n_, 0x1.921FB54442D18p0, yd_);                    \
         const double x2_ = x_ * x_;                                                       \
         const double m_ = M_SELECT(x_, x2_);                                              \

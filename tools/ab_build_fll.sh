@@ -9,7 +9,7 @@ root=$(cd "$(dirname "$0")/.." && pwd)
 pkg=$root/qpsk-modulator-demodulator_amd
 src=$pkg/csrc/qpsk_fll.hip
 if [ $# -gt 0 ] && [ -f "$1" ]; then src=$(cd "$(dirname "$1")" && pwd)/$(basename "$1"); shift; fi
-flags="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -I$root/include -I$pkg/csrc -mllvm -amdgpu-sched-strategy=iterative-ilp"
+flags="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -I$root/include -I$pkg/csrc -mllvm -misched=ilpmin"
 mkdir -p "$pkg/_build/ab"
 /opt/rocm/bin/hipcc $flags "$@" -c "$src" -o "$pkg/_build/ab/fll_$name.o" 2> /dev/null
 objs=$(ls "$pkg"/_build/*.o | grep -v '/qpsk_fll.o$')
