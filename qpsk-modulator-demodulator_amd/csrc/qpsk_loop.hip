@@ -59,6 +59,9 @@ constexpr int kMir = 4;
 #ifndef QPSK_COSTAS_UNROLL2
 #define QPSK_COSTAS_UNROLL2 1
 #endif
+#ifndef QPSK_LOOP_ROTB
+#define QPSK_LOOP_ROTB 1   // decisions-only Costas -> decode slots when no symbols are written
+#endif
 #ifndef QPSK_MM_LSHLADD
 #define QPSK_MM_LSHLADD 1
 #endif
@@ -155,14 +158,19 @@ struct RowStride { static constexpr int value = CAP + 1; };
 // TRIG 0: the portable sincos table (qpsk_sincos.h), heads and tails; TRIG 1:
 // glibc's __sincostab in the split form's two layouts (qpsk_glibc_trig.h:
 // do_sin rows at 0, do_cos rows at 440), no tails
-template <int SPW, int CAP, int KB, int TRIG>
+// ROTB: the Costas wave hands the decode wave only the two decisions (the
+// sign bytes of +-1.0, 2 B per symbol) instead of the rotated symbol (8 B)
+// when no symbols are written out: at C3 the workgroup drops from 125 KB to
+// 114 KB of LDS, and two matched-filter workgroups of the next pipelined
+// call fit beside it instead of one
+template <int SPW, int CAP, int KB, int TRIG, bool ROTB>
 struct LoopLds {
     static constexpr int RS = RowStride<CAP>::value;
     double tab[TRIG ? 880 : 1024];  // sincos table head, at LDS offset 0 so
     double tab_lo[TRIG ? 2 : 1024]; // the table index is the whole address; tail (floats, widened)
     f2 mf[SPW * Ring<KB>::row];    // sample ring   [stream][mirror | 4 rounds x KB]
     sym_t sym[2 * SPW * RS];       // M&M -> Costas [slot][stream][RS] (see sym_t)
-    f2 rot[2 * SPW * RS];          // Costas -> decode
+    typename std::conditional<ROTB, uint16_t, f2>::type rot[2 * SPW * RS];   // Costas -> decode
     int cnt[4 * SPW + 4];          // symbols produced by the M&M in round r: cnt[r & 3];
                                    // cnt[4*SPW + (r & 3)] = their minimum over the batch
 };
@@ -172,7 +180,8 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     constexpr int kRing = Ring<KB>::len, kRowS = Ring<KB>::row;
     // one LDS object only: a second __shared__ object would make hipcc drain the
     // loader's LDS-DMA before touching it (cdna_hip_programming.md §5)
-    __shared__ LoopLds<SPW, CAP, KB, TRIG> L;
+    constexpr bool ROTB = QPSK_LOOP_ROTB && !SYMS;
+    __shared__ LoopLds<SPW, CAP, KB, TRIG, ROTB> L;
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -647,7 +656,8 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             const int slot = (r - 1) & 1;
             const int m = mine ? L.cnt[((r - 1) & 3) * SPW + lane] : 0;
             for (int k = 0; k < m; ++k) {
-                L.rot[(slot * SPW + lane) * L.RS + k] = sym_to_f2(L.sym[(slot * SPW + lane) * L.RS + k]);
+                if constexpr (ROTB) L.rot[(slot * SPW + lane) * L.RS + k] = 0;
+                else L.rot[(slot * SPW + lane) * L.RS + k] = sym_to_f2(L.sym[(slot * SPW + lane) * L.RS + k]);
             }
         }
         return;
@@ -698,7 +708,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             const int m = cmine ? L.cnt[((r - 1) & 3) * SPW + cl] : 0;
             const sym_t *in = L.sym + (slot * SPW + cl) * L.RS;
             // (TRIG 1: both lanes of a stream store the same value to the same slot)
-            f2 *out = L.rot + (slot * SPW + cl) * L.RS;
+            auto *out = L.rot + (slot * SPW + cl) * L.RS;
             d2 y;
             // CostasLoopQpsk.cs:63-92: double NCO, float I/O (y widened to double).
             // HUGE: theta may exceed the table reduction's range (|theta| <= 2^40,
@@ -746,7 +756,14 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 // is tn - 2pi above pi and tn + 2pi below -pi
                 const double tw = tn - copysign(kTwoPi, tn);
                 theta = fabs(tn) > kPi ? tw : tn;
-                out[k] = f2{ri, rq};
+                if constexpr (ROTB) {
+                    // the decisions' sign bytes (byte 3 of the high words of +-1.0)
+                    const uint32_t eih = static_cast<uint32_t>(__builtin_bit_cast(uint64_t, ei) >> 32);
+                    const uint32_t eqh = static_cast<uint32_t>(__builtin_bit_cast(uint64_t, eq) >> 32);
+                    out[k] = static_cast<uint16_t>(__builtin_amdgcn_perm(eqh, eih, 0x0c0c0703u));
+                } else {
+                    out[k] = f2{ri, rq};
+                }
                 y = yn;
             };
             const double theta0 = theta, freq0 = freq;
@@ -839,18 +856,26 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         if (r < 2) continue;
         const int slot = (r - 2) & 1;
         const int m = dmine ? L.cnt[((r - 2) & 3) * SPW + lane] : 0;
-        const f2 *in = L.rot + (slot * SPW + lane) * L.RS;
+        const auto *in = L.rot + (slot * SPW + lane) * L.RS;
         for (int k = 0; k < m; ++k) {
-            const f2 rr = in[k];
-            if (SYMS) {
-                if (ncs < a.syms_cap) syms[ncs] = rr;
-                else err |= 2;
+            float ei, eq;
+            if constexpr (ROTB) {
+                const uint32_t db = in[k];
+                ei = (db & 0x80u) ? -1.0f : 1.0f;
+                eq = (db & 0x8000u) ? -1.0f : 1.0f;
+            } else {
+                const f2 rr = in[k];
+                if (SYMS) {
+                    if (ncs < a.syms_cap) syms[ncs] = rr;
+                    else err |= 2;
+                }
+                // decision (QPSKDeModulator.cs:379-407)
+                ei = rr.x >= 0.0f ? 1.0f : -1.0f;
+                eq = rr.y >= 0.0f ? 1.0f : -1.0f;
             }
             ++ncs;
             if (MODE == kModeDemodulate) {
-                // decision + differential decode (QPSKDeModulator.cs:379-407, 304-337)
-                const float ei = rr.x >= 0.0f ? 1.0f : -1.0f;
-                const float eq = rr.y >= 0.0f ? 1.0f : -1.0f;
+                // differential decode (QPSKDeModulator.cs:379-407, 304-337)
                 uint32_t b2;
                 bool emit = true;
                 if (DIFF) {
