@@ -39,6 +39,9 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ int lds_slot(int i) { return i + ((i >> 6) << 3); }
 constexpr int lds_slots(int n) { return n + ((n >> 6) << 3) + 8; }
 
+#ifndef QPSK_FIR_DIRECT_STORE
+#define QPSK_FIR_DIRECT_STORE 1   // outputs stored from the accumulators (no LDS transpose)
+#endif
 #ifndef QPSK_FIR_THREADS
 #define QPSK_FIR_THREADS 256   // A/B builds: 128 / 64 (1024- / 512-output tiles)
 #endif
@@ -242,6 +245,49 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, const float *hr
     const int grp = tid / W, r = tid % W;
     f2 acc[Q];
     fir_core<T, W, Q>(lds + 72 * grp + r, r, hrev, acc);
+#if QPSK_FIR_DIRECT_STORE
+    // Each output straight from its accumulator: output t0 + W q of lane r of
+    // group grp (t0 = 64 grp + r), so a wave's store covers eight 64-B runs.
+    // No LDS transpose, no barrier after the compute: the workgroup's LDS is
+    // free as soon as its waves are done.  An output whose fast value is not
+    // finite had a NaN or Inf in its window and is recomputed with the
+    // reference's full products; a finite one had none, and then the fast
+    // value is the exact one (fir_exact_one), so the check is per output.
+    if (ph_wg) p2 = __builtin_amdgcn_s_memtime();
+    {
+        f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride + a.y_offset;
+        const int o0 = 64 * grp + r;
+        unsigned bad = 0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int64_t go = tile0 + o0 + W * q;
+            const bool nf = fir_nonfinite(acc[q].x) | fir_nonfinite(acc[q].y);
+            bad |= static_cast<unsigned>(nf) << q;
+            if (go < n) y[go] = acc[q];
+        }
+        if (ph_wg) {
+            const unsigned long long p3 = __builtin_amdgcn_s_memtime();
+            unsigned long long *ph = a.phases + 8 * shared_cu;
+            atomicAdd(ph + 0, p1 - p0);
+            atomicAdd(ph + 1, p2 - p1);
+            atomicAdd(ph + 2, p3 - p2);
+            atomicAdd(ph + 3, 1ull);
+        }
+        if (__builtin_expect(bad != 0, 0)) {
+#pragma unroll 1
+            for (int q = 0; q < Q; ++q) {
+                const int64_t go = tile0 + o0 + W * q;   // output sample
+                if (!((bad >> q) & 1u) || go >= n) continue;
+                const int64_t w0 = go - (T - 1);         // its oldest window sample
+                auto xs = [&](int k) -> f2 {
+                    const int64_t g = w0 + k;
+                    return g < 0 ? hist[T - 1 + g] : x[g];
+                };
+                y[go] = fir_exact_one(xs, hrev, T, W);
+            }
+        }
+    }
+#else
     __syncthreads();
     if (ph_wg) p2 = __builtin_amdgcn_s_memtime();
 #pragma unroll
@@ -294,6 +340,7 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, const float *hr
             y[go] = fir_exact_one(xs, hrev, T, W);
         }
     }
+#endif
     if (clk_wg) {
         const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = wall_clock64();
         atomicAdd(a.clk, c1 - c0);
