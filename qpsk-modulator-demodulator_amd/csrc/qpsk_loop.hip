@@ -87,6 +87,9 @@ constexpr int kCapSps8 = 14;
 // 128-sample rounds at sps >= 8 (variant 4): lag_max = 64 needs
 // (CAP - 1)(sps - 0.1) >= KB + 4 + 64 -> CAP = 26
 constexpr int kCap128Sps8 = 26;
+// 32-sample rounds at sps >= 8 (variant 5, 64 streams: every lane of the
+// stage waves busy): lag_max = 16 needs (CAP - 1)(sps - 0.1) >= 52 -> CAP = 8
+constexpr int kCap32Sps8 = 8;
 typedef double d2 __attribute__((ext_vector_type(2)));
 
 // M&M -> Costas symbol slots: doubles (default; the M&M wave has them widened
@@ -314,7 +317,8 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         if (NR > 1) issue(1);
         for (int r = 0; r <= NR + 1; ++r) {
             STAMP(ta);
-            if (r + 1 < NR) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPW) : "memory");
+            // round r's loads done, round r + 1's (SPW, the counter holds 63) in flight
+            if (r + 1 < NR) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPW < 63 ? SPW : 63) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             ACC(t_wait, ta);
             STAMP(tb);
@@ -947,8 +951,12 @@ static int launch_loop_spw_t(const LoopArgs &a, const LoopParams &P, int mode, h
 
 template <int SPW, int CAP, int KB>
 static int launch_loop_spw(const LoopArgs &a, const LoopParams &P, int mode, hipStream_t stream) {
-    return P.costas_trig ? launch_loop_spw_t<SPW, CAP, KB, 1>(a, P, mode, stream)
-                         : launch_loop_spw_t<SPW, CAP, KB, 0>(a, P, mode, stream);
+    if constexpr (SPW > 32) {   // the split glibc sincos needs both wave halves per stream
+        return launch_loop_spw_t<SPW, CAP, KB, 0>(a, P, mode, stream);
+    } else {
+        return P.costas_trig ? launch_loop_spw_t<SPW, CAP, KB, 1>(a, P, mode, stream)
+                             : launch_loop_spw_t<SPW, CAP, KB, 0>(a, P, mode, stream);
+    }
 }
 
 int launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant, hipStream_t stream) {
@@ -967,6 +975,11 @@ int launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant, h
         return launch_loop_spw<16, kCap128Sps2, 128>(a, P, mode, stream);
     else if (variant == 4 && P.sps >= 8.0)
         return launch_loop_spw<24, kCap128Sps8, 128>(a, P, mode, stream);
+    else if (variant == 5 && P.sps >= 8.0 && !P.costas_trig)
+        // 64 streams x 32-sample rounds: every stage-wave lane busy, 105 KB of
+        // LDS (a 4-round ring of 64-sample rounds for 64 streams would take
+        // 133 KB alone); measured, not the default
+        return launch_loop_spw<64, kCap32Sps8, 32>(a, P, mode, stream);
     else if (P.sps >= 8.0)
         return launch_loop_spw<32, kCapSps8, 64>(a, P, mode, stream);
     else if (P.sps >= 4.0)

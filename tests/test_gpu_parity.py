@@ -91,14 +91,14 @@ def test_single_call_bit_exact(sps, span):
 
 
 @pytest.mark.parametrize("sps,span", K.CONFIGS)
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_chunked_ragged_calls_bit_exact(sps, span, variant):
     """Every loop-kernel shape (qpsk_demod_params.loop_variant) on ragged calls,
     including 0/1/2/3-sample calls and calls longer than a round."""
     if variant == 3 and sps < 2:
         pytest.skip("16 x 128 needs sps >= 2 (the launcher never picks it below)")
-    if variant == 4 and sps < 8:
-        pytest.skip("24 x 128 is the sps >= 8 shape (below it the launcher falls back to auto)")
+    if variant in (4, 5) and sps < 8:
+        pytest.skip("24 x 128 and 64 x 32 are sps >= 8 shapes (below it the launcher falls back to auto)")
     iq = K.batch_signals(4, seed0=20, sps=sps, span=span, n_bits=2400, snr_db=14)
     n = iq.shape[1] // 2
     rng = np.random.default_rng(sps)
