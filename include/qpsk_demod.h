@@ -46,8 +46,11 @@ extern "C" {
 
 /* status flags (qpsk_demod_status; a host-memory process() call returns the
  * matching error code when its own call raised one) */
-#define QPSK_STATUS_CARRY_OVERFLOW 1u    /* symbol-sync queue kept > 256 samples (sps > 250):
-                                            the reference keeps them all (MuellerMuller.cs:123-133) */
+#define QPSK_STATUS_CARRY_OVERFLOW 1u    /* symbol-sync queue kept > 256 samples: the queue
+                                            holds <= 3 samples between calls at any sps, more
+                                            only when the M&M stops on output capacity (sps
+                                            below ~1); the reference keeps them all
+                                            (MuellerMuller.cs:123-133) */
 #define QPSK_STATUS_OUTPUT_TRUNCATED 2u  /* a bit / symbol row hit its capacity */
 #define QPSK_STATUS_NONFINITE_TIMING 4u  /* a NaN/Inf sample reached the M&M timing loop: the
                                             reference's (int)Math.Floor(NaN) = 0 pins baseIndex

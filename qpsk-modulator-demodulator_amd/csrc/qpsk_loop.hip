@@ -65,6 +65,14 @@ constexpr int kMir = 4;
 #ifndef QPSK_MM_LSHLADD
 #define QPSK_MM_LSHLADD 1
 #endif
+// Costas wrap as |tn| - 2pi with tn's sign xored in, and -(eq*mi) as a sign
+// flip of mi's high word: 2 VALU fewer per symbol (49 -> 47), bit-exact in the
+// GPU suite, but measured no faster: C3 +0.5 %, C2 -1.1 % (the M&M wave, which
+// paces C2, slows as the Costas wave's LDS reads bunch up), C4 -0.4 %
+// (profiles/r04_costas_wrap_ab.txt); off
+#ifndef QPSK_COSTAS_WRAP_ABS
+#define QPSK_COSTAS_WRAP_ABS 0
+#endif
 
 #ifndef QPSK_RING_PAD
 #define QPSK_RING_PAD 0
@@ -695,6 +703,9 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         // otherwise each iteration rebuilds some from SGPR halves (VOP3 reads
         // one scalar operand), which costs issue slots on an issue-bound chain
         asm volatile("" : "+v"(ca), "+v"(cb), "+v"(kTwoPi), "+v"(kPi));
+        // the sign bit in a VGPR (v_bitop3_b32 takes no literal)
+        uint32_t sgn_v = 0x80000000u;
+        asm volatile("" : "+v"(sgn_v));
         asm volatile("" : "+v"(K.INV), "+v"(K.SH), "+v"(K.P1), "+v"(K.P2));
         asm volatile("" : "+v"(K.S3), "+v"(K.S5), "+v"(K.C4), "+v"(K.C6));
 #ifdef QPSK_LOOP_STAMPS
@@ -753,13 +764,39 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 // rounds the same exact difference as the reference's subtraction
                 const double ei = ri >= 0.0f ? 1.0 : -1.0;
                 const double eq = rq >= 0.0f ? 1.0 : -1.0;
+#if QPSK_COSTAS_WRAP_ABS
+                // -(eq*mi) = mi with its sign bit flipped unless eq = -1: one
+                // v_bitop3 on mi's high word (mi is dead after it, so the pair
+                // stays in place) instead of a multiply by a +-1.0 pair built
+                // around a copied zero word
+                const uint64_t mib = __builtin_bit_cast(uint64_t, mi);
+                const uint32_t eqhw = static_cast<uint32_t>(__builtin_bit_cast(uint64_t, eq) >> 32);
+                const uint32_t nmh = static_cast<uint32_t>(mib >> 32) ^ (~eqhw & sgn_v);
+                const double pe = fma(ei, mq, __builtin_bit_cast(double, (static_cast<uint64_t>(nmh) << 32) |
+                                                                             static_cast<uint32_t>(mib)));
+#else
                 const double pe = fma(ei, mq, -(eq * mi));
+#endif
                 freq = freq + cb * pe;
                 const double tn = theta + (freq + ca * pe);
+#if QPSK_COSTAS_WRAP_ABS
+                // single +-2pi wrap (:89-91) as a select: above pi tn - 2pi =
+                // |tn| - 2pi, below -pi tn + 2pi = -(|tn| - 2pi) (rounding is
+                // sign-symmetric), so the wrapped value is |tn| - 2pi (one add
+                // with an abs modifier) with tn's sign bit xored into its high
+                // word (one v_bitop3); the select takes the halves separately,
+                // so no register pair has to be assembled
+                const double am = fabs(tn) - kTwoPi;
+                const uint64_t tnb = __builtin_bit_cast(uint64_t, tn), amb = __builtin_bit_cast(uint64_t, am);
+                const uint32_t twh = static_cast<uint32_t>(amb >> 32) ^ (static_cast<uint32_t>(tnb >> 32) & sgn_v);
+                const double tw = __builtin_bit_cast(double, (static_cast<uint64_t>(twh) << 32) | static_cast<uint32_t>(amb));
+                theta = fabs(tn) > kPi ? tw : tn;
+#else
                 // single +-2pi wrap (:89-91) as a select: tn - copysign(2pi, tn)
                 // is tn - 2pi above pi and tn + 2pi below -pi
                 const double tw = tn - copysign(kTwoPi, tn);
                 theta = fabs(tn) > kPi ? tw : tn;
+#endif
                 if constexpr (ROTB) {
                     // the decisions' sign bytes (byte 3 of the high words of +-1.0)
                     const uint32_t eih = static_cast<uint32_t>(__builtin_bit_cast(uint64_t, ei) >> 32);

@@ -1018,7 +1018,7 @@ int flush_deferred(qpsk_demod *h) {
 int host_call_status(qpsk_demod *h) {
     const uint32_t f = *h->h_flags;
     if (f & QPSK_STATUS_CARRY_OVERFLOW)
-        return fail(QPSK_ERR_STATE, "symbol-sync queue over 256 retained samples (sps > 250?)");
+        return fail(QPSK_ERR_STATE, "symbol-sync queue over 256 retained samples (output capacity hit: sps below ~1?)");
     if (f & QPSK_STATUS_OUTPUT_TRUNCATED) return fail(QPSK_ERR_CAPACITY, "output row truncated");
     if (f & QPSK_STATUS_NONFINITE_TIMING)
         return fail(QPSK_ERR_STATE, "non-finite sample reached the symbol timing loop");

@@ -15,8 +15,10 @@
 
 namespace qpsk {
 
-// retained M&M samples between calls: normally sps + 3 at most (the samples
-// from the next symbol's base on), so 256 covers sps up to ~250
+// retained M&M samples between calls: at most 3 whatever sps is
+// (MuellerMuller.cs:123-133 drops min(baseIndex - 1, count - 3), and the loop
+// leaves baseIndex >= count - 2); more only when the output capacity stops the
+// loop early (sps below ~1, where DeModulate's n-symbol span is too small)
 constexpr int kCarryMax = 256;
 constexpr int kMfPrefix = 256;     // MF buffer prefix that receives the carry
 constexpr int kFllTaps = 40;       // QPSKDeModulator.cs:35

@@ -114,12 +114,14 @@ def test_chunked_ragged_calls_bit_exact(sps, span, variant):
     assert_same(gpu_run(iq, calls, sps, span, loop_variant=variant), oracle_run(iq, calls, sps, span))
 
 
-@pytest.mark.parametrize("sps,span", [(30, 6), (100, 4), (200, 2)])
+@pytest.mark.parametrize("sps,span", [(30, 6), (100, 4), (200, 2), (300, 2), (1000, 1)])
 def test_large_sps_multi_call_bit_exact(sps, span):
-    """Samples per symbol up to 200 (the reference's own testFullDemodChain
-    runs sps 30): the M&M queue retained between calls (up to sps + 3
-    samples, MuellerMuller.cs:123-133) rides in the 256-sample carry, across
-    calls shorter than one symbol too."""
+    """Samples per symbol up to 1000 (the reference's own testFullDemodChain
+    runs sps 30), across calls shorter than one symbol too.  The queue the
+    M&M keeps between calls is at most 3 samples whatever sps is
+    (MuellerMuller.cs:123-133 drops min(baseIndex - 1, count - 3)); a symbol
+    base past the end carries over as the state's base offset, not as
+    samples."""
     iq = K.batch_signals(3, seed0=25, sps=sps, span=span, n_bits=300, snr_db=18)
     n = iq.shape[1] // 2
     calls, left, k = [], np.full(3, n), 0
