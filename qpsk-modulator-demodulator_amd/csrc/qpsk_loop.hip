@@ -98,6 +98,9 @@ constexpr int kCap128Sps8 = 26;
 // 32-sample rounds at sps >= 8 (variant 5, 64 streams: every lane of the
 // stage waves busy): lag_max = 16 needs (CAP - 1)(sps - 0.1) >= 52 -> CAP = 8
 constexpr int kCap32Sps8 = 8;
+// 256-sample rounds at sps >= 8 (variant 6): lag_max = 128 needs
+// (CAP - 1)(sps - 0.1) >= KB + 4 + 128 -> CAP = 51
+constexpr int kCap256Sps8 = 51;
 typedef double d2 __attribute__((ext_vector_type(2)));
 
 // M&M -> Costas symbol slots: doubles (default; the M&M wave has them widened
@@ -186,8 +189,13 @@ struct LoopLds {
                                    // cnt[4*SPW + (r & 3)] = their minimum over the batch
 };
 
-template <int MODE, bool DIFF, bool SYMS, int SPW, int CAP, int KB, int TRIG>
+// SPW = streams (LDS rows) per workgroup; ACT >= SPW = lanes of the stage
+// waves that run the chains: lanes SPW <= l < ACT shadow the workgroup's first
+// stream on its own LDS rows (same addresses as lane 0, same values written),
+// so a shape with few rows (long rounds) still keeps its waves' lanes busy
+template <int MODE, bool DIFF, bool SYMS, int SPW, int CAP, int KB, int TRIG, int ACT>
 __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
+    static_assert(ACT >= SPW && ACT <= (TRIG ? 32 : 64), "active lanes");
     constexpr int kRing = Ring<KB>::len, kRowS = Ring<KB>::row;
     // one LDS object only: a second __shared__ object would make hipcc drain the
     // loader's LDS-DMA before touching it (cdna_hip_programming.md §5)
@@ -229,8 +237,9 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     // runs these loops 10-50 % slower per symbol than one with 20 or more
     // (profiles/archive/r02_loop_probe_lanes.txt), so small batches keep SPW lanes busy
     const bool real = lane < nvalid;            // owns stream s: writes its results
-    const bool valid = lane < SPW;              // computes stream sc
+    const bool valid = lane < ACT;              // computes stream sc
     const int sc = real ? s : blk_s0;
+    const int rowl = lane < SPW ? lane : 0;     // LDS row of stream sc
 
     // ---- per-stream queue geometry (every wave: lane l <-> stream sc)
     int n = 0, cnt = 0, R = 0, d = 0;
@@ -265,9 +274,11 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
 #endif
     if (wave == 0) {
         // ============================================================ loader
-        // one glds instruction = KB/2 lanes x 16 B = one stream's round (8*KB bytes)
+        // one glds instruction = KB/2 lanes x 16 B = one stream's round (8*KB
+        // bytes); KB = 256: NI = 2 instructions of 64 lanes (128 samples each)
+        constexpr int NI = KB > 128 ? KB / 128 : 1;
         const int64_t org = valid ? sc * a.mf_stride + kMfPrefix - R - d : 0;
-        const int c2 = 2 * (lane % (KB / 2));
+        const int c2 = 2 * (lane % (KB / 2 < 64 ? KB / 2 : 64));
         const f2 *mf = reinterpret_cast<const f2 *>(a.mf);
         const bool lo_half = lane < KB / 2;
         // Fast path (every round but a stream's last): byte offsets of each
@@ -300,22 +311,29 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const char *rb = reinterpret_cast<const char *>(wg_mf + static_cast<int64_t>(r) * KB);
 #pragma unroll
                 for (int j = 0; j < SPW; ++j)
-                    if (lo_half)
-                        __builtin_amdgcn_global_load_lds((glb_void_t *)(rb + voff[j]),
-                                                         (lds_void_t *)(L.mf + j * kRowS + kMir + roff), 16, 0, 0);
+#pragma unroll
+                    for (int h = 0; h < NI; ++h)
+                        if (lo_half)
+                            __builtin_amdgcn_global_load_lds((glb_void_t *)(rb + voff[j] + 1024 * h),
+                                                             (lds_void_t *)(L.mf + j * kRowS + kMir + roff + 128 * h),
+                                                             16, 0, 0);
                 return;
             }
 #pragma unroll 4
             for (int j = 0; j < SPW; ++j) {
                 const int c = __builtin_amdgcn_readlane(cnt, j);
                 const int64_t o = readlane64(org, j);
-                int p = r * KB + c2;
-                // past the stream's end: read a harmless in-row pair (never used);
-                // a pair straddling the end reads one sample of row slack
-                if (p >= c) p = 0;
-                if (lo_half)
-                    __builtin_amdgcn_global_load_lds((glb_void_t *)(mf + o + p),
-                                                     (lds_void_t *)(L.mf + j * kRowS + kMir + roff), 16, 0, 0);
+#pragma unroll
+                for (int h = 0; h < NI; ++h) {
+                    int p = r * KB + c2 + 128 * h;
+                    // past the stream's end: read a harmless in-row pair (never used);
+                    // a pair straddling the end reads one sample of row slack
+                    if (p >= c) p = 0;
+                    if (lo_half)
+                        __builtin_amdgcn_global_load_lds((glb_void_t *)(mf + o + p),
+                                                         (lds_void_t *)(L.mf + j * kRowS + kMir + roff + 128 * h),
+                                                         16, 0, 0);
+                }
             }
         };
 #ifdef QPSK_LOOP_STAMPS
@@ -325,8 +343,8 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         if (NR > 1) issue(1);
         for (int r = 0; r <= NR + 1; ++r) {
             STAMP(ta);
-            // round r's loads done, round r + 1's (SPW, the counter holds 63) in flight
-            if (r + 1 < NR) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPW < 63 ? SPW : 63) : "memory");
+            // round r's loads done, round r + 1's (SPW * NI, the counter holds 63) in flight
+            if (r + 1 < NR) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPW * NI < 63 ? SPW * NI : 63) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             ACC(t_wait, ta);
             STAMP(tb);
@@ -371,7 +389,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         const int cap = n;                          // output span = 2n floats (QPSKDeModulator.cs:366)
         int nsym = 0;
         bool stop = !mine;                          // capacity reached (MuellerMuller.cs:101-102)
-        f2 *row = L.mf + lane * kRowS;
+        f2 *row = L.mf + rowl * kRowS;
         // taps x[b-1..b+2] of physical index b: contiguous thanks to the mirror
         auto taps = [&](int b) -> const f2 * { return row + kMir - 3 + ((b + 2) & (kRing - 1)); };
         // Timing runs in the reference's coordinates: t = baseIndex + mu with
@@ -433,13 +451,13 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             ACC(c_bar, tb);
             if (r >= NR) continue;
             STAMP(tl);
-            if ((r & 3) == 0 && r > 0 && mine) {
+            if ((r & 3) == 0 && r > 0 && mine && lane < SPW) {
                 // mirror = last 4 samples of the ring (round r-1, already consumed)
                 row[0] = row[kMir + kRing - 4]; row[1] = row[kMir + kRing - 3];
                 row[2] = row[kMir + kRing - 2]; row[3] = row[kMir + kRing - 1];
             }
             const int rend = (r + 1) * KB < cnt ? (r + 1) * KB : cnt;
-            sym_t *out = L.sym + ((r & 1) * SPW + lane) * L.RS;
+            sym_t *out = L.sym + ((r & 1) * SPW + rowl) * L.RS;
             int kmax = stop ? 0 : (cap - nsym < CAP ? cap - nsym : CAP);
             int k = 0, kuni = 0;
             lds_f2 *tp = (lds_f2 *)taps(base);
@@ -719,11 +737,12 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             STAMP(tl);
             const int slot = (r - 1) & 1;
             const int mlo = __builtin_amdgcn_readfirstlane(L.cnt[4 * SPW + ((r - 1) & 3)]);
-            if (cl >= SPW) continue;   // exec = the batch's lanes for the whole round
-            const int m = cmine ? L.cnt[((r - 1) & 3) * SPW + cl] : 0;
-            const sym_t *in = L.sym + (slot * SPW + cl) * L.RS;
+            if (cl >= ACT) continue;   // exec = the batch's lanes for the whole round
+            const int crow = cl < SPW ? cl : 0;
+            const int m = cmine ? L.cnt[((r - 1) & 3) * SPW + crow] : 0;
+            const sym_t *in = L.sym + (slot * SPW + crow) * L.RS;
             // (TRIG 1: both lanes of a stream store the same value to the same slot)
-            auto *out = L.rot + (slot * SPW + cl) * L.RS;
+            auto *out = L.rot + (slot * SPW + crow) * L.RS;
             d2 y;
             // CostasLoopQpsk.cs:63-92: double NCO, float I/O (y widened to double).
             // HUGE: theta may exceed the table reduction's range (|theta| <= 2^40,
@@ -968,31 +987,31 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     if (a.n_bits) a.n_bits[s] = MODE == kModeDemodulate ? nbits : 0;
 }
 
-template <int SPW, int CAP, int KB, int TRIG>
+template <int SPW, int CAP, int KB, int TRIG, int ACT>
 static int launch_loop_spw_t(const LoopArgs &a, const LoopParams &P, int mode, hipStream_t stream) {
     dim3 grid((a.S + SPW - 1) / SPW), block(256);
     const bool syms = a.syms != nullptr;
     const bool diff = P.differential != 0;
     if (mode == kModeConstellation)
-        hipLaunchKernelGGL((loop_kernel<kModeConstellation, false, true, SPW, CAP, KB, TRIG>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeConstellation, false, true, SPW, CAP, KB, TRIG, ACT>), grid, block, 0, stream, a, P);
     else if (diff && syms)
-        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, true, SPW, CAP, KB, TRIG>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, true, SPW, CAP, KB, TRIG, ACT>), grid, block, 0, stream, a, P);
     else if (diff)
-        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, false, SPW, CAP, KB, TRIG>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, true, false, SPW, CAP, KB, TRIG, ACT>), grid, block, 0, stream, a, P);
     else if (syms)
-        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, true, SPW, CAP, KB, TRIG>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, true, SPW, CAP, KB, TRIG, ACT>), grid, block, 0, stream, a, P);
     else
-        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, false, SPW, CAP, KB, TRIG>), grid, block, 0, stream, a, P);
+        hipLaunchKernelGGL((loop_kernel<kModeDemodulate, false, false, SPW, CAP, KB, TRIG, ACT>), grid, block, 0, stream, a, P);
     return static_cast<int>(grid.x);
 }
 
-template <int SPW, int CAP, int KB>
+template <int SPW, int CAP, int KB, int ACT = SPW>
 static int launch_loop_spw(const LoopArgs &a, const LoopParams &P, int mode, hipStream_t stream) {
-    if constexpr (SPW > 32) {   // the split glibc sincos needs both wave halves per stream
-        return launch_loop_spw_t<SPW, CAP, KB, 0>(a, P, mode, stream);
+    if constexpr (ACT > 32) {   // the split glibc sincos needs both wave halves per stream
+        return launch_loop_spw_t<SPW, CAP, KB, 0, ACT>(a, P, mode, stream);
     } else {
-        return P.costas_trig ? launch_loop_spw_t<SPW, CAP, KB, 1>(a, P, mode, stream)
-                             : launch_loop_spw_t<SPW, CAP, KB, 0>(a, P, mode, stream);
+        return P.costas_trig ? launch_loop_spw_t<SPW, CAP, KB, 1, ACT>(a, P, mode, stream)
+                             : launch_loop_spw_t<SPW, CAP, KB, 0, ACT>(a, P, mode, stream);
     }
 }
 
@@ -1017,6 +1036,10 @@ int launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant, h
         // LDS (a 4-round ring of 64-sample rounds for 64 streams would take
         // 133 KB alone); measured, not the default
         return launch_loop_spw<64, kCap32Sps8, 32>(a, P, mode, stream);
+    else if (variant == 6 && P.sps >= 8.0)
+        // 12 streams x 256-sample rounds, 32 busy lanes (20 shadow lanes on
+        // row 0): a quarter of the rounds of 32 x 64, 135 KB of LDS
+        return launch_loop_spw<12, kCap256Sps8, 256, 32>(a, P, mode, stream);
     else if (P.sps >= 8.0)
         return launch_loop_spw<32, kCapSps8, 64>(a, P, mode, stream);
     else if (P.sps >= 4.0)

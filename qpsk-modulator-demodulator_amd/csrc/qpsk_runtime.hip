@@ -533,9 +533,9 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
         delete h;
         return fail(QPSK_ERR_ARGUMENT, "vector_lanes must be 1, 4, 8 or 16");
     }
-    if (p->loop_variant < 0 || p->loop_variant > 5) {
+    if (p->loop_variant < 0 || p->loop_variant > 6) {
         delete h;
-        return fail(QPSK_ERR_ARGUMENT, "loop_variant must be 0..5");
+        return fail(QPSK_ERR_ARGUMENT, "loop_variant must be 0..6");
     }
     std::string err;
     int rc = design_loops(p->sample_rate, p->symbol_rate, p->rrc_alpha, p->rrc_span,
