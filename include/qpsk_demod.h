@@ -87,8 +87,9 @@ typedef struct qpsk_demod_params {
                                        1 = 16 streams x 64-sample rounds, 2 = 32 x 64,
                                        3 = 16 x 128 (sps >= 2 only), 4 = 24 x 128 (sps >= 8
                                        only, else auto), 5 = 64 x 32 (sps >= 8 and
-                                       costas_trig 0 only, else auto), 6 = 12 x 256
-                                       (sps >= 8 only, else auto); results are
+                                       costas_trig 0 only, else auto), 6 = 12 x 256,
+                                       7 = 6 x 512 (both sps >= 8 only, else auto;
+                                       32 busy lanes); results are
                                        identical */
     int32_t iq_balance;             /* 1 = IQ_Balancer.Process (IQ Balancer.cs:15-25) on every
                                        sample before the FLL / matched filter; 0 (default) =

@@ -101,6 +101,9 @@ constexpr int kCap32Sps8 = 8;
 // 256-sample rounds at sps >= 8 (variant 6): lag_max = 128 needs
 // (CAP - 1)(sps - 0.1) >= KB + 4 + 128 -> CAP = 51
 constexpr int kCap256Sps8 = 51;
+// 512-sample rounds at sps >= 8 (variant 7): lag_max = 256 needs CAP >= 99;
+// 100 makes the row stride (CAP + 1) odd
+constexpr int kCap512Sps8 = 100;
 typedef double d2 __attribute__((ext_vector_type(2)));
 
 // M&M -> Costas symbol slots: doubles (default; the M&M wave has them widened
@@ -1040,6 +1043,9 @@ int launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant, h
         // 12 streams x 256-sample rounds, 32 busy lanes (20 shadow lanes on
         // row 0): a quarter of the rounds of 32 x 64, 135 KB of LDS
         return launch_loop_spw<12, kCap256Sps8, 256, 32>(a, P, mode, stream);
+    else if (variant == 7 && P.sps >= 8.0)
+        // 6 streams x 512-sample rounds, 26 shadow lanes: 137 KB of LDS
+        return launch_loop_spw<6, kCap512Sps8, 512, 32>(a, P, mode, stream);
     else if (P.sps >= 8.0)
         return launch_loop_spw<32, kCapSps8, 64>(a, P, mode, stream);
     else if (P.sps >= 4.0)

@@ -533,9 +533,9 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
         delete h;
         return fail(QPSK_ERR_ARGUMENT, "vector_lanes must be 1, 4, 8 or 16");
     }
-    if (p->loop_variant < 0 || p->loop_variant > 6) {
+    if (p->loop_variant < 0 || p->loop_variant > 7) {
         delete h;
-        return fail(QPSK_ERR_ARGUMENT, "loop_variant must be 0..6");
+        return fail(QPSK_ERR_ARGUMENT, "loop_variant must be 0..7");
     }
     std::string err;
     int rc = design_loops(p->sample_rate, p->symbol_rate, p->rrc_alpha, p->rrc_span,
@@ -599,8 +599,19 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
     if (hipDeviceGetAttribute(&h->wall_khz, hipDeviceAttributeWallClockRate, p->device) != hipSuccess ||
         h->wall_khz <= 0)
         h->wall_khz = 100000;
-    if (h->loop_variant == 0 && h->lp.sps >= 8.0 && h->cus > 0 && (h->S + 23) / 24 <= h->cus / 2)
-        h->loop_variant = 4;
+    // Round 4: long rounds with shadow lanes (6 x 512, 12 x 256: 32 busy lanes,
+    // a quarter / half of the per-round bookkeeping per symbol of 24 x 128)
+    // beat it wherever they fit the chip in one pass, at sps >= 8, A/B on one
+    // MI355X (profiles/r04_loop_long_rounds_ab.txt): 256 streams 13.6 -> 14.4
+    // GSa/s (C2), 1024: 48.5 / 51.2 / 54.5 (24 x 128 / 12 x 256 / 6 x 512),
+    // 2048: 88.4 / 99.3 (32 x 64: 74.6).  Above 12 x 256's one pass (4096
+    // streams, C4) the 32 x 64 default stays: more workgroups than CUs, and
+    // half-empty waves cost the FIR beside them issue slots
+    if (h->loop_variant == 0 && h->lp.sps >= 8.0 && h->cus > 0) {
+        if ((h->S + 5) / 6 <= h->cus) h->loop_variant = 7;
+        else if ((h->S + 11) / 12 <= h->cus) h->loop_variant = 6;
+        else if ((h->S + 23) / 24 <= h->cus / 2) h->loop_variant = 4;
+    }
     h->use_gate = qpsk_pipeline_gate_enabled() == 1;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipStreamCreate failed"));

@@ -193,7 +193,7 @@ def test_sincos_tables_match_independent_model():
     assert hi_p == ref and lo_p == ref_lo
 
 
-@pytest.mark.parametrize("kw", [dict(loop_variant=7), dict(loop_variant=-1), dict(vector_lanes=3),
+@pytest.mark.parametrize("kw", [dict(loop_variant=8), dict(loop_variant=-1), dict(vector_lanes=3),
                                 dict(max_samples_per_call=0)])
 def test_create_rejects_bad_knobs_before_touching_a_device(kw):
     """Argument checks run before any HIP call, so they hold on a CPU-only host."""

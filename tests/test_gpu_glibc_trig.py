@@ -38,7 +38,7 @@ def test_glibc_trig_single_call_bit_exact(sps, span):
     assert_same(gpu_run(iq, calls, sps, span, **GL), oracle_run(iq, calls, sps, span, **LIBM))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 6, 7])
 def test_glibc_trig_ragged_chunks_every_loop_shape(variant):
     sps, span = 8, 8
     iq = K.batch_signals(4, seed0=910, sps=sps, span=span, n_bits=4000, snr_db=14)

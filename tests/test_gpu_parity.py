@@ -91,13 +91,13 @@ def test_single_call_bit_exact(sps, span):
 
 
 @pytest.mark.parametrize("sps,span", K.CONFIGS)
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_chunked_ragged_calls_bit_exact(sps, span, variant):
     """Every loop-kernel shape (qpsk_demod_params.loop_variant) on ragged calls,
     including 0/1/2/3-sample calls and calls longer than a round."""
     if variant == 3 and sps < 2:
         pytest.skip("16 x 128 needs sps >= 2 (the launcher never picks it below)")
-    if variant in (4, 5, 6) and sps < 8:
+    if variant in (4, 5, 6, 7) and sps < 8:
         pytest.skip("24 x 128, 64 x 32 and 12 x 256 are sps >= 8 shapes (below it the launcher falls back to auto)")
     iq = K.batch_signals(4, seed0=20, sps=sps, span=span, n_bits=2400, snr_db=14)
     n = iq.shape[1] // 2
@@ -114,7 +114,7 @@ def test_chunked_ragged_calls_bit_exact(sps, span, variant):
     assert_same(gpu_run(iq, calls, sps, span, loop_variant=variant), oracle_run(iq, calls, sps, span))
 
 
-@pytest.mark.parametrize("variant", [4, 6])
+@pytest.mark.parametrize("variant", [4, 6, 7])
 def test_long_round_shapes_many_streams_bit_exact(variant):
     """The 128- and 256-sample-round shapes over several workgroups (30
     streams: 2 x 15 rows of 24, or 3 x 10 rows of 12 with 22 shadow lanes each)
