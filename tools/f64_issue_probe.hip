@@ -55,22 +55,28 @@ int main() {
     const int iters = 1000;
     const char *names[] = {"v_add_f64 (2 src)", "v_mul_f64 (2 src)", "v_fma_f64 (3 VGPR pairs)",
                            "v_fmac_f64 (2 src + dst)", "v_fma_f64 (SGPR addend)", "v_fma_f64 dependent chain"};
-    auto run = [&](auto kfn, int v) {
-        hipLaunchKernelGGL(kfn, dim3(256), dim3(256), 0, 0, cyc, sink, 10, 1e-7);
+    // blocks = 256 x 4 waves: one wave on every SIMD; blocks = 1, 64 threads:
+    // one wave on an otherwise idle GPU (isa_bench's setting)
+    auto run = [&](auto kfn, int v, int blocks, int threads) {
+        hipLaunchKernelGGL(kfn, dim3(blocks), dim3(threads), 0, 0, cyc, sink, 10, 1e-7);
         hipDeviceSynchronize();
-        hipLaunchKernelGGL(kfn, dim3(256), dim3(256), 0, 0, cyc, sink, iters, 1e-7);
+        hipLaunchKernelGGL(kfn, dim3(blocks), dim3(threads), 0, 0, cyc, sink, iters, 1e-7);
         hipDeviceSynchronize();
         long long h[1024];
         hipMemcpy(h, cyc, sizeof h, hipMemcpyDeviceToHost);
+        const int nw = blocks * threads / 64;
         double s = 0;
-        for (int i = 0; i < 1024; ++i) s += h[i];
-        printf("%-30s %.2f cycles per instruction\n", names[v], s / 1024 / (iters * 64.0));
+        for (int i = 0; i < nw; ++i) s += h[(i / (threads / 64)) * 4 + i % (threads / 64)];
+        printf("%-30s %4d waves: %.2f cycles per instruction\n", names[v], nw, s / nw / (iters * 64.0));
     };
-    run(kern<0>, 0);
-    run(kern<1>, 1);
-    run(kern<2>, 2);
-    run(kern<3>, 3);
-    run(kern<4>, 4);
-    run(kern<5>, 5);
+    for (int cfg = 0; cfg < 2; ++cfg) {
+        const int blocks = cfg ? 1 : 256, threads = cfg ? 64 : 256;
+        run(kern<0>, 0, blocks, threads);
+        run(kern<1>, 1, blocks, threads);
+        run(kern<2>, 2, blocks, threads);
+        run(kern<3>, 3, blocks, threads);
+        run(kern<4>, 4, blocks, threads);
+        run(kern<5>, 5, blocks, threads);
+    }
     return 0;
 }
