@@ -183,6 +183,12 @@ int qpsk_demod_process_async(qpsk_demod *h, int32_t mode, const float *iq, int64
 /* 1 if handles created now use the residency gate, 0 if the environment turns
  * it off (the list above); needs no device. */
 int qpsk_pipeline_gate_enabled(void);
+/* The symbol-loop shape qpsk_demod_create picks for loop_variant = 0 (auto):
+ * at sps >= 8, 7 (6 streams x 512-sample rounds) while ceil(S/6) <= cus, else
+ * 6 (12 x 256) while ceil(S/12) <= cus, else 4 (24 x 128) while ceil(S/24) <=
+ * cus/2, else 0 (the launcher's default for the sps: 32 x 64 at sps >= 2).
+ * A requested variant != 0 is returned unchanged.  Needs no device. */
+int32_t qpsk_demod_pick_loop_variant(int32_t requested, int32_t n_streams, double sps, int32_t cus);
 /* OR of the QPSK_STATUS_* flags raised since the last qpsk_demod_status call
  * (waits for every queued call), then cleared.  0 = every call so far stayed
  * inside the reference's defined behaviour. */

@@ -607,11 +607,7 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
     // 2048: 88.4 / 99.3 (32 x 64: 74.6).  Above 12 x 256's one pass (4096
     // streams, C4) the 32 x 64 default stays: more workgroups than CUs, and
     // half-empty waves cost the FIR beside them issue slots
-    if (h->loop_variant == 0 && h->lp.sps >= 8.0 && h->cus > 0) {
-        if ((h->S + 5) / 6 <= h->cus) h->loop_variant = 7;
-        else if ((h->S + 11) / 12 <= h->cus) h->loop_variant = 6;
-        else if ((h->S + 23) / 24 <= h->cus / 2) h->loop_variant = 4;
-    }
+    h->loop_variant = qpsk_demod_pick_loop_variant(h->loop_variant, h->S, h->lp.sps, h->cus);
     h->use_gate = qpsk_pipeline_gate_enabled() == 1;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipStreamCreate failed"));
@@ -1345,6 +1341,15 @@ int qpsk_demod_set_state(qpsk_demod *h, const void *host_buf, int64_t buf_bytes)
     p += S * 8 * H;
     HIP_TRY(hipMemcpy(h->d_fll_delay, p, S * 8 * 2 * kFllTaps, hipMemcpyHostToDevice));
     return QPSK_OK;
+}
+
+int32_t qpsk_demod_pick_loop_variant(int32_t requested, int32_t n_streams, double sps, int32_t cus) {
+    if (requested != 0 || !(sps >= 8.0) || cus <= 0 || n_streams <= 0) return requested;
+    const int64_t S = n_streams;
+    if ((S + 5) / 6 <= cus) return 7;
+    if ((S + 11) / 12 <= cus) return 6;
+    if ((S + 23) / 24 <= cus / 2) return 4;
+    return 0;
 }
 
 // Residency gate default (process_async_one).  hipStreamWaitValue64 cannot

@@ -180,6 +180,8 @@ def lib():
     L.qpsk_demod_get_state.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     L.qpsk_demod_set_state.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     L.qpsk_pipeline_gate_enabled.restype = C.c_int
+    L.qpsk_demod_pick_loop_variant.argtypes = [C.c_int32, C.c_int32, C.c_double, C.c_int32]
+    L.qpsk_demod_pick_loop_variant.restype = C.c_int32
     L.qpsk_demod_enable_fir_phases.argtypes = [C.c_void_p, C.c_int32]
     L.qpsk_demod_fir_phases.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     L.qpsk_framer_create.argtypes = [C.c_int32, _u8p, C.c_int32, _u8p, C.c_int32, C.c_int64,
@@ -219,7 +221,8 @@ EXPORTED_SYMBOLS = [
     "qpsk_demod_kernel_clocks",
     "qpsk_demod_rrc_taps",
     "qpsk_demod_gains", "qpsk_demod_fll_taps", "qpsk_demod_state_bytes", "qpsk_demod_get_state",
-    "qpsk_demod_set_state", "qpsk_pipeline_gate_enabled", "qpsk_demod_enable_fir_phases",
+    "qpsk_demod_set_state", "qpsk_pipeline_gate_enabled", "qpsk_demod_pick_loop_variant",
+    "qpsk_demod_enable_fir_phases",
     "qpsk_demod_fir_phases", "qpsk_demod_design", "qpsk_framer_create", "qpsk_framer_destroy",
     "qpsk_framer_set_markers", "qpsk_framer_push", "qpsk_framer_dev_create",
     "qpsk_framer_dev_destroy", "qpsk_framer_dev_set_stream", "qpsk_framer_dev_set_markers",

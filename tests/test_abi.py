@@ -236,3 +236,26 @@ def test_pipeline_gate_predicate(monkeypatch, env, want):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     assert Q.lib().qpsk_pipeline_gate_enabled() == want
+
+
+@pytest.mark.parametrize("requested,S,sps,cus,want", [
+    (0, 256, 8.0, 256, 7),      # C2: 43 workgroups of 6 x 512
+    (0, 1536, 8.0, 256, 7),     # 256 workgroups: still one pass
+    (0, 1537, 8.0, 256, 6),     # 12 x 256
+    (0, 2048, 8.0, 256, 6),
+    (0, 3072, 8.0, 256, 6),
+    (0, 3073, 8.0, 256, 0),     # 24 x 128 would need 129 > cus / 2 workgroups
+    (0, 4096, 8.0, 256, 0),     # C4 shard: the 32 x 64 default
+    (0, 8192, 8.0, 256, 0),     # C5
+    (0, 3073, 8.0, 1024, 7),    # a larger chip keeps the long rounds
+    (0, 256, 4.0, 256, 0),      # sps < 8 (C3): the launcher's default
+    (0, 256, 7.99, 256, 0),
+    (0, 256, 30.0, 256, 7),     # the reference's testFullDemodChain sps
+    (2, 256, 8.0, 256, 2),      # an explicit shape is kept
+    (0, 256, 8.0, 0, 0),        # unknown CU count
+])
+def test_auto_loop_shape(requested, S, sps, cus, want):
+    """The loop shape qpsk_demod_create picks (long rounds with
+    shadow lanes while they fit the chip in one pass, A/B-measured at 256,
+    1024, 2048 and 4096 streams); evaluated without a device."""
+    assert Q.lib().qpsk_demod_pick_loop_variant(requested, S, sps, cus) == want
