@@ -16,8 +16,14 @@ RRC).  Streams are independent (QPSKDeModulator.cs:20-73), so ranks shard
 streams with no data-path collective ("scaling": "weak": every rank owns its
 own C3-shaped batch); the only collectives are the MAX of the timed region and
 the sums of the parity / BER counters after it.  The other configs run after
-the headline as `sub_records` (N=1: C2 and C5; N>1: the C4 shard shape, 4096
-streams/GPU at sps 8, plus the RCCL scatter/gather leg of SURVEY.md 8e).
+the headline as `sub_records` (N=1: C2, the C4 shard, C5 and C3 with the
+glibc-exact Costas trig; N>1: the C4 shard shape, 4096 streams/GPU at sps 8,
+plus the RCCL scatter/gather leg of SURVEY.md 8e).
+
+stdout carries ONE compact JSON line (<= LINE_MAX_BYTES: the driver's keys,
+roofline, cpu_baseline, parity counts, GPU and CPU BER, per sub-record the
+same); the full record (per-launch statistics, clocks, FIR phase samples,
+framer, host ring) goes to the --detail side file, named in the line.
 
 After each config's timed region (never inside it) the timed handle itself is
 checked: one call from the initial state on every stream, whose bit rows are
@@ -66,6 +72,10 @@ CONFIGS = {
                name="C4 shard: 4096 streams/GPU x 2^20 complex samples, sps=8, 65-tap RRC"),
     "c5": dict(streams=8192, sps=8, span=8, impaired=True, fll=True,
                name="C5: 8192 streams x 2^20, +-5 kHz CFO + 4-tap multipath + 20 dB, FLL on"),
+    # C3 with the Costas loop's own trig restated exactly (CostasLoopQpsk.cs:69-70:
+    # glibc sin/cos): bit-exact by construction, not by measurement
+    "c3_glibc": dict(streams=4096, sps=4, span=32, impaired=False, fll=False, costas_trig=1,
+                     name="C3, glibc-exact Costas sin/cos (costas_trig=1)"),
 }
 
 
@@ -184,13 +194,18 @@ def pick_streams(S, n_cover, tail=64):
     return list(range(head)) + list(range(S - tail, S))
 
 
+BER_STREAMS = 32      # leading streams of every rank's shard that BER is counted on
+
+
 def cpu_leg(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, n, budget_s, threads, single_streams=8,
             n_cover=None, costas_trig=0):
     """CPU baseline + parity at scale: the oracle (glibc trig) on the host
     cores over a time-bounded subset of the timed batch, timed, and its bit
     rows / symbols compared with the GPU's rows of the same streams.
     n_cover: a fixed stream count instead of the time budget (N > 1: every
-    rank checks the first 8 and the last 64 streams of its shard)."""
+    rank checks the first 32 and the last 64 streams of its shard).
+    Also returns the oracle's own bit rows (and counts) of the leading
+    min(S, BER_STREAMS) streams, for the CPU side of the BER comparison."""
     import numpy as np
     import torch
     import oracle as O
@@ -206,7 +221,7 @@ def cpu_leg(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, n, budget_s, thre
     per_stream = dt1 / ns1
     eff = min(threads, cpu_quota() or threads)
     if n_cover is None:
-        n_cover = max(min(S, 64 + 8), int(budget_s * eff / per_stream))
+        n_cover = max(min(S, 64 + BER_STREAMS), int(budget_s * eff / per_stream))
     idx = pick_streams(S, n_cover)
     host = rows_to_host(iq, idx)
     want_syms = syms_dev is not None
@@ -243,7 +258,9 @@ def cpu_leg(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, n, budget_s, thre
               "max_row_offset_GiB": round(idx[-1] * iq.stride(0) * 4 / 2**30, 2)}
     if not want_syms:
         parity["note"] = "bits only: no HBM left for a symbol copy of the whole batch"
-    return cpu, parity
+    k = min(S, BER_STREAMS)
+    assert idx[:k] == list(range(k))
+    return cpu, parity, (rb[:k], rnb[:k])
 
 
 def portable_check(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, idx, costas_trig=0):
@@ -314,9 +331,11 @@ def ber_after_lock(bits_dev, nbits_dev, tx_dev, n_streams, skip_bits=8000, windo
     or an error in it) or whose offset changes inside them (last `key_bits`
     misaligned) are reported as `lost_windows`, not as bit errors."""
     import numpy as np
-    nb = nbits_dev[:n_streams].cpu().numpy()
-    bits = bits_dev[:n_streams].cpu().numpy()
-    tx = tx_dev[:n_streams].cpu().numpy()
+
+    def host(t):
+        t = t[:n_streams]
+        return t.cpu().numpy() if hasattr(t, "cpu") else np.asarray(t)
+    nb, bits, tx = host(nbits_dev), host(bits_dev), host(tx_dev)
     errs = total = lost = slips = 0
     for s in range(n_streams):
         rx = np.unpackbits(bits[s])[: int(nb[s])]
@@ -637,6 +656,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
     import qpsk_amd as Q
 
     cfg = dict(CONFIGS[key])
+    trig = cfg.get("costas_trig", args.costas_trig)
     S = args.streams or cfg["streams"]
     n = args.samples
     sps, span = cfg["sps"], cfg["span"]
@@ -651,7 +671,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
                     esn0_db=20.0 if cfg["impaired"] else None, device=dev.index)
     iq, tx = Q.synth_generate(S, n, FS, rs, first_stream=lo, **synth_kw)
     p = Q.params(FS, rs, ALPHA, span, enable_fll=cfg["fll"], device=dev.index, max_samples_per_call=n,
-                 loop_variant=args.loop_variant, costas_trig=args.costas_trig)
+                 loop_variant=args.loop_variant, costas_trig=trig)
     demod = Q.BatchDemodulator(S, p)
     fresh_state = demod.get_state()   # for the parity / BER call (no second handle: C5 needs ~256 GiB)
     # a real stream (torch's legacy default is handle 0, which the C ABI reads
@@ -704,6 +724,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
     libm_bad = libm_streams = 0
     steady_bad = steady_n = 0
     steady_ex, steady_freq = [], []
+    cerrs = ctotal = clost = cslips = ber_cpu_ok = 0
     if not args.timed_only and not args.no_parity:
         # the last timed call's rows, before anything overwrites them: the first
         # and last two streams and the four whose Costas loop runs fastest (the
@@ -749,19 +770,25 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
         demod.set_state(fresh_state)
         demod.process_device(iq, n, bits, nbits, syms_dev=syms, n_syms_dev=nsyms)
         torch.cuda.synchronize(dev)
-        errs, total_bits, lost, slips = ber_after_lock(bits, nbits, tx, min(S, 32))
+        errs, total_bits, lost, slips = ber_after_lock(bits, nbits, tx, min(S, BER_STREAMS))
         if not args.no_parity:
             idx = [0, 1, S - 2, S - 1] if S >= 4 else list(range(S))
-            bad_bits, bad_syms = portable_check(iq, bits, nbits, syms, nsyms, cfg, idx, args.costas_trig)
+            bad_bits, bad_syms = portable_check(iq, bits, nbits, syms, nsyms, cfg, idx, trig)
             n_port = len(idx)
             if not args.no_cpu_baseline:
                 # every rank: the libm oracle on its own shard (N = 1: as many
                 # streams as the CPU budget allows; N > 1: the first 8 and last
                 # 64 of the shard, on this rank's share of the host threads)
                 threads = args.cpu_threads or max(1, (os.cpu_count() or 1) // world)
-                cpu, par = cpu_leg(iq, bits, nbits, syms, nsyms, cfg, n, args.cpu_seconds, threads,
-                                   n_cover=None if world == 1 else min(S, 72), costas_trig=args.costas_trig)
+                cpu, par, (rb, rnb) = cpu_leg(iq, bits, nbits, syms, nsyms, cfg, n, args.cpu_seconds, threads,
+                                              n_cover=None if world == 1 else min(S, 64 + BER_STREAMS),
+                                              costas_trig=trig)
                 libm_bad, libm_streams = par["mismatching_streams"], par["streams"]
+                # the same BER count on the CPU oracle's own bit rows of the
+                # same streams ("BER vs CPU ref"): equal to the GPU's iff the
+                # rows are, so a nonzero clean-channel BER is the algorithm's
+                cerrs, ctotal, clost, cslips = ber_after_lock(rb, rnb, tx, min(S, BER_STREAMS))
+                ber_cpu_ok = 1
                 if rank == 0:
                     rec["cpu_baseline"], rec["parity_vs_libm_oracle"] = cpu, par
         del syms, nsyms
@@ -772,9 +799,9 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
         del gathered
         rec["output_gather"] = og
     t_max, (errs, total_bits, lost, slips, bad_bits, bad_syms, n_port, libm_bad, libm_streams,
-            steady_bad, steady_n) = reduce_stats(
+            steady_bad, steady_n, cerrs, ctotal, clost, cslips, ber_cpu_ok) = reduce_stats(
         elapsed, [errs, total_bits, lost, slips, bad_bits, bad_syms, n_port, libm_bad, libm_streams,
-                  steady_bad, steady_n],
+                  steady_bad, steady_n, cerrs, ctotal, clost, cslips, ber_cpu_ok],
         device=dev if nccl else None)
     if world > 1 and "parity_vs_libm_oracle" in rec:
         par = rec["parity_vs_libm_oracle"]
@@ -826,7 +853,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
                    "streams_per_gpu": S, "samples_per_stream": n,
                    "sps": sps, "taps": span * sps + 1, "fll": cfg["fll"],
                    "parallelism": f"stream-shard x{world}",
-                   "costas_trig": "glibc sin/cos (bit-exact)" if args.costas_trig else
+                   "costas_trig": "glibc sin/cos (bit-exact)" if trig else
                                   "portable table sincos (<= 1 ulp from glibc)",
                    "calls": "serial" if args.serial_calls else
                             f"pipelined (front/back stage overlap, depth {demod.pipeline_depth()})"},
@@ -836,7 +863,12 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
         "ber_after_lock": {"bit_errors": errs, "bits": total_bits,
                            "ber": (errs / total_bits) if total_bits else None,
                            "lost_windows": lost, "symbol_slips": slips,
-                           "streams": min(S, 32) * world},
+                           "streams": min(S, BER_STREAMS) * world},
+        # the same counter over the CPU oracle's rows of the same streams
+        "ber_cpu": ({"bit_errors": cerrs, "bits": ctotal, "ber": (cerrs / ctotal) if ctotal else None,
+                     "lost_windows": clost, "symbol_slips": cslips,
+                     "equal": (cerrs, ctotal, clost, cslips) == (errs, total_bits, lost, slips)}
+                    if ber_cpu_ok == world else "not measured"),
         "parity_steady_state": (
             "not checked" if (args.no_parity or args.timed_only) else
             {"streams": steady_n, "mismatching_streams": steady_bad, "calls": warmup + steps,
@@ -849,7 +881,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
         "parity_vs_portable_oracle": (
             "not checked" if (args.no_parity or args.timed_only) else
             {"streams": n_port, "bit_mismatch_streams": bad_bits, "symbol_mismatch_streams": bad_syms,
-             "oracle": "glibc trig (libm)" if args.costas_trig else "portable trig",
+             "oracle": "glibc trig (libm)" if trig else "portable trig",
              "note": "first and last two streams of every rank's shard; bits and symbols must be "
                      "bit-identical (the oracle runs the GPU's own Costas trig)"}),
         **rec,
@@ -904,6 +936,93 @@ def split_gather_leg(args, rank, world, dev, S=256):
     return rec
 
 
+# ---------------------------------------------------------------------------
+# the stdout line: what the driver parses, bounded; everything else goes to
+# the side file (--detail, default bench_detail.json next to bench.py)
+# ---------------------------------------------------------------------------
+LINE_MAX_BYTES = 12_000
+HEAD_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+             "scaling", "vs_baseline", "dtype", "data", "config")
+ROOF_KEYS = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "valu_frac", "clock_ghz")
+CPU_KEYS = ("value", "unit", "cores", "kind", "single_core", "cpu_quota_cpus", "sample")
+KERNEL_KEYS = ("ms", "achieved", "frac", "valu_frac_unfused_at_clock", "cycles_per_symbol",
+               "cycles_per_sample", "clock_ghz_median")
+BER_KEYS = ("ber", "bit_errors", "bits", "lost_windows", "symbol_slips", "streams", "equal")
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and d.get(k) is not None}
+
+
+def _parity_counts(rec):
+    """Every parity leg of one record as counts (streams checked, streams
+    that differ from the oracle)."""
+    out = {}
+    lib = rec.get("parity_vs_libm_oracle")
+    if isinstance(lib, dict):
+        out["libm_oracle"] = {"streams": lib["streams"], "mismatching": lib["mismatching_streams"]}
+        if lib.get("max_sym_err") is not None:
+            out["libm_oracle"]["max_sym_err"] = lib["max_sym_err"]
+            out["libm_oracle"]["sym_tol"] = lib["sym_tol"]
+    port = rec.get("parity_vs_portable_oracle")
+    if isinstance(port, dict):
+        out["same_trig_oracle"] = {"streams": port["streams"], "bit_mismatching": port["bit_mismatch_streams"],
+                                   "symbol_mismatching": port["symbol_mismatch_streams"]}
+    st = rec.get("parity_steady_state")
+    if isinstance(st, dict):
+        out["steady_state"] = {"streams": st["streams"], "mismatching": st["mismatching_streams"],
+                               "calls": st["calls"]}
+    return out or "not checked"
+
+
+def _compact_body(rec):
+    body = {"roofline": _pick(rec.get("roofline"), ROOF_KEYS) or None,
+            "kernels": {k: _pick(v, KERNEL_KEYS) for k, v in (rec.get("rooflines") or {}).items()},
+            "stages_ms": rec.get("stages_ms"),
+            "cpu_baseline": _pick(rec.get("cpu_baseline"), CPU_KEYS) or None,
+            "parity": _parity_counts(rec),
+            "ber": _pick(rec.get("ber_after_lock"), BER_KEYS)}
+    bc = rec.get("ber_cpu")
+    body["ber_cpu"] = _pick(bc, BER_KEYS) if isinstance(bc, dict) else bc
+    for k in ("output_gather", "split_gather"):
+        if k in rec:
+            body[k] = rec[k]
+    return body
+
+
+def compact_record(out, detail_name):
+    """The one stdout JSON line: the driver's keys, the headline's roofline,
+    cpu_baseline, parity counts and BER (GPU and CPU), and per sub-record the
+    same, compact.  Launch statistics, clock ranges, FIR phase samples, the
+    framer and host-ring passes live in the detail file only."""
+    line = {k: out[k] for k in HEAD_KEYS if k in out}
+    line.update(_compact_body(out))
+    subs = {}
+    for key, r in (out.get("sub_records") or {}).items():
+        s = {k: r[k] for k in ("value", "ms_per_step", "steps", "warmup") if k in r}
+        s["workload"] = r.get("config", {}).get("workload")
+        s.update(_compact_body(r))
+        subs[key] = s
+    if subs:
+        line["sub_records"] = subs
+    line["detail"] = detail_name
+    return line
+
+
+def dump_line(line):
+    """Serialise the stdout line within LINE_MAX_BYTES: if it would be
+    longer, the sub-records lose their per-kernel tables, then everything but
+    value and ms_per_step (the detail file keeps all of it)."""
+    s = json.dumps(line, separators=(",", ":"))
+    for keep in (lambda k: k != "kernels", lambda k: k in ("value", "ms_per_step", "workload")):
+        if len(s) <= LINE_MAX_BYTES or "sub_records" not in line:
+            break
+        line = dict(line, sub_records={key: {k: v for k, v in r.items() if keep(k)}
+                                       for key, r in line["sub_records"].items()})
+        s = json.dumps(line, separators=(",", ":"))
+    return s
+
+
 def spawn_ranks(args):
     """--gpus N without a launcher: run N ranks under torch.distributed.run in a
     child process (this process never touches the GPU) and return its status."""
@@ -923,7 +1042,7 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
                     help="headline workload (default C3, the largest single-GPU config)")
     ap.add_argument("--sub-configs", default="auto",
-                    help="comma list run after the headline as sub_records; 'auto' = c2,c4,c5 at N=1 "
+                    help="comma list run after the headline as sub_records; 'auto' = c2,c4,c5,c3_glibc at N=1 "
                          "(c4: the per-GPU shard of BASELINE's 8-GPU config, the N = 1 point of its "
                          "curve), c4 at N>1; 'none' = headline only")
     ap.add_argument("--sub-steps", type=int, default=20)
@@ -954,6 +1073,9 @@ def main():
                     help="synchronous process() per step (no front/back stage overlap)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="every rank uses cuda:0 (rehearsal only; numbers meaningless)")
+    ap.add_argument("--detail", default="",
+                    help="side file for the full record (launch stats, clocks, FIR phases, framer, "
+                         "host ring); default bench_detail.json next to bench.py")
     args = ap.parse_args()
     if args.timed_only:
         args.no_parity = args.no_framer = args.no_split_gather = True
@@ -988,7 +1110,7 @@ def main():
     out = run_config(args.config, args, rank, world, dev, args.steps, args.warmup, headline=True)
     subs = args.sub_configs
     if subs == "auto":
-        subs = "c2,c4,c5" if world == 1 else "c4"
+        subs = "c2,c4,c5,c3_glibc" if world == 1 else "c4"
     sub = {}
     for key in [k for k in subs.split(",") if k and k != "none" and k != args.config]:
         r = run_config(key, args, rank, world, dev, args.sub_steps, 1, headline=False)
@@ -1001,7 +1123,14 @@ def main():
         out["split_gather"] = split_gather_leg(args, rank, world, dev)
     sys.stdout.flush()
     if rank == 0:
-        os.write(json_fd, (json.dumps(out) + "\n").encode())
+        detail = os.path.abspath(args.detail or os.path.join(ROOT, "bench_detail.json"))
+        try:
+            with open(detail, "w") as f:
+                json.dump(out, f, indent=1)
+            name = os.path.relpath(detail, ROOT) if detail.startswith(ROOT + os.sep) else detail
+        except OSError as e:
+            name = f"not written ({e})"
+        os.write(json_fd, (dump_line(compact_record(out, name)) + "\n").encode())
     if world > 1:
         dist.destroy_process_group()
 
