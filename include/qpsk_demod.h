@@ -86,8 +86,8 @@ typedef struct qpsk_demod_params {
     int32_t loop_variant;           /* symbol-loop kernel shape: 0 = auto,
                                        1 = 16 streams x 64-sample rounds, 2 = 32 x 64,
                                        3 = 16 x 128 (sps >= 2 only), 4 = 24 x 128 (sps >= 8
-                                       only, else auto), 5 = 64 x 32 (sps >= 8 and
-                                       costas_trig 0 only, else auto), 6 = 12 x 256,
+                                       only, else auto), 5 = retired (64 x 32,
+                                       measured slower; runs as auto), 6 = 12 x 256,
                                        7 = 6 x 512 (both sps >= 8 only, else auto;
                                        32 busy lanes); results are
                                        identical */
@@ -185,8 +185,9 @@ int qpsk_demod_process_async(qpsk_demod *h, int32_t mode, const float *iq, int64
 int qpsk_pipeline_gate_enabled(void);
 /* The symbol-loop shape qpsk_demod_create picks for loop_variant = 0 (auto):
  * at sps >= 8, 7 (6 streams x 512-sample rounds) while ceil(S/6) <= cus, else
- * 6 (12 x 256) while ceil(S/12) <= cus, else 4 (24 x 128) while ceil(S/24) <=
- * cus/2, else 0 (the launcher's default for the sps: 32 x 64 at sps >= 2).
+ * 6 (12 x 256) while ceil(S/12) <= cus, else 0 (the launcher's default for the
+ * sps: 32 x 64 at sps >= 2).  (24 x 128, variant 4, needed ceil(S/24) <= cus/2,
+ * which no batch past the 12 x 256 bound meets; it is only picked on request.)
  * A requested variant != 0 is returned unchanged.  Needs no device. */
 int32_t qpsk_demod_pick_loop_variant(int32_t requested, int32_t n_streams, double sps, int32_t cus);
 /* OR of the QPSK_STATUS_* flags raised since the last qpsk_demod_status call

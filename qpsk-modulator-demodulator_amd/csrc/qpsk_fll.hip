@@ -58,11 +58,6 @@
 #include "qpsk_kernels.h"
 #include "qpsk_sincosf.h"
 
-#ifndef QPSK_FLL_PROBE
-#define QPSK_FLL_PROBE 0   // diagnostic bits (timing only, results wrong): 1 no sincos, 2 no
-                           // partial sums, 4 no broadcast, 8 no redo; 0 = product
-#endif
-
 namespace qpsk {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -287,11 +282,6 @@ void fll_sys_kernel(FllArgs a, FllParams P) {
         float sn, cs;
         if constexpr (decltype(first)::value) {
             qpsk_sincosf_glibc(phase, &sn, &cs);
-#if QPSK_FLL_PROBE & 1
-        } else if (true) {   // diagnostic: no sincos on the chain
-            sn = phase * 0.5f;
-            cs = 1.0f - phase;
-#endif
         } else {
             // a kept result has |phase| <= 2pi (or NaN): the branch-free form
             qpsk_sincosf_glibc_fast_k(phase, &sn, &cs, sign_v);
@@ -311,19 +301,12 @@ void fll_sys_kernel(FllArgs a, FllParams P) {
         y[t0 + u] = xm;
         f2 R4, I4;
         band_prod(TA[4], TB[4], xm, R4, I4);
-#if QPSK_FLL_PROBE & 2
-        PR = f2{0.f, 0.f}; PI = f2{0.f, 0.f};   // diagnostic: no partial-sum work
-#endif
         const f2 ar = PR + R4, ai = PI + I4;
         SR = f2{shr2(SR.x) + ar.x, shr2(SR.y) + ar.y};
         SI = f2{shr2(SI.x) + ai.x, shr2(SI.y) + ai.y};
         // lane 7 holds the filter outputs of sample t: {pow upper, pow lower}
         const f2 pw = SR * SR + SI * SI;
-#if QPSK_FLL_PROBE & 4
-        const float err = pw.y - pw.x;   // diagnostic: no broadcast
-#else
         const float err = bcast7(pw.y - pw.x, odd);
-#endif
         freq = freq + beta * err;
         phase = phase + freq;   // alpha == 0 (file comment)
         if constexpr (decltype(exact)::value) {
@@ -334,12 +317,10 @@ void fll_sys_kernel(FllArgs a, FllParams P) {
             amax = fmaxf(amax, fabsf(phase));   // NaN never wraps or clamps: ignored
             fmx = fmaxf(fmx, fabsf(freq));
         }
-#if !(QPSK_FLL_PROBE & 2)
         if constexpr (decltype(reg)::value)
             partial([&](int k) -> f2 { return k == 32 ? xmv[0] : X[k]; }, u + 1);
         else
             partial(ring_at(t0), u + 1);
-#endif
     };
     // 8 samples of every stream of the wave, no masks
     typedef __attribute__((address_space(3))) f4 lds_f4;
@@ -361,7 +342,7 @@ void fll_sys_kernel(FllArgs a, FllParams P) {
 #pragma unroll
         for (int u = 1; u < 8; ++u)
             step(in[u], t0, u, std::false_type{}, std::false_type{}, amax, fmx, std::true_type{}, X, xmv);
-        if (!(QPSK_FLL_PROBE & 8) && __builtin_expect(__ballot((amax > two_pi) | (fmx > fmax_)) != 0, 0)) {
+        if (__builtin_expect(__ballot((amax > two_pi) | (fmx > fmax_)) != 0, 0)) {
             // some stream's phase needed a wrap or its frequency a clamp: redo
             // from the block start (its outputs are rewritten)
             phase = ph0; freq = fr0; SR = sr0; SI = si0; PR = pr0; PI = pi0;

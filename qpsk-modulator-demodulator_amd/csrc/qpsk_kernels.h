@@ -100,8 +100,8 @@ struct LoopArgs {
     // holds its CUs (qpsk_runtime.hip, process_async_one)
     unsigned long long *resident;
     unsigned long long *clk;   // clock sample of the M&M wave (ClkSample) or nullptr
-    // or nullptr: cu_map[cu_key()] is 1 while a workgroup of this launch holds
-    // that CU (FIR phase sample, FirArgs.phases)
+    // or nullptr: cu_map[cu_key()] counts the workgroups of this launch that
+    // hold that CU (FIR phase sample, FirArgs.phases)
     unsigned *cu_map;
 };
 

@@ -39,13 +39,8 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ int lds_slot(int i) { return i + ((i >> 6) << 3); }
 constexpr int lds_slots(int n) { return n + ((n >> 6) << 3) + 8; }
 
-#ifndef QPSK_FIR_DIRECT_STORE
-#define QPSK_FIR_DIRECT_STORE 1   // outputs stored from the accumulators (no LDS transpose)
-#endif
-#ifndef QPSK_FIR_THREADS
-#define QPSK_FIR_THREADS 256   // A/B builds: 128 / 64 (1024- / 512-output tiles)
-#endif
-constexpr int kFirThreads = QPSK_FIR_THREADS;
+// 2048-output tiles; 1024- and 512-output tiles measured the same
+constexpr int kFirThreads = 256;
 constexpr unsigned kKtLastWgs = 8192;
 
 // One output of the tile with the reference's full complex products
@@ -245,7 +240,6 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, const float *hr
     const int grp = tid / W, r = tid % W;
     f2 acc[Q];
     fir_core<T, W, Q>(lds + 72 * grp + r, r, hrev, acc);
-#if QPSK_FIR_DIRECT_STORE
     // Each output straight from its accumulator: output t0 + W q of lane r of
     // group grp (t0 = 64 grp + r), so a wave's store covers eight 64-B runs.
     // No LDS transpose, no barrier after the compute: the workgroup's LDS is
@@ -287,60 +281,6 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, const float *hr
             }
         }
     }
-#else
-    __syncthreads();
-    if (ph_wg) p2 = __builtin_amdgcn_s_memtime();
-#pragma unroll
-    for (int q = 0; q < Q; ++q) lds[72 * grp + r + W * q] = acc[q];
-    __syncthreads();
-
-    // A NaN or Inf sample anywhere in the tile (halo included) leaves some
-    // fast output non-finite; the stores below watch for that, and such a tile
-    // is recomputed with the reference's full products straight from HBM.
-    int bad = 0;
-    f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride + a.y_offset;
-    if constexpr (VEC) {
-        for (int p = tid; p < TILE / 2; p += NT) {
-            const int64_t g = tile0 + 2 * p;
-            const f4 v = *reinterpret_cast<const f4 *>(&lds[lds_slot(2 * p)]);
-            bad |= fir_nonfinite(v.x) | fir_nonfinite(v.y) | fir_nonfinite(v.z) | fir_nonfinite(v.w);
-            if (g + 1 < n) {
-                *reinterpret_cast<f4 *>(y + g) = v;
-            } else if (g < n) {
-                y[g] = f2{v.x, v.y};
-            }
-        }
-    } else {
-        for (int i = tid; i < TILE; i += NT) {
-            const int64_t g = tile0 + i;
-            const f2 v = lds[lds_slot(i)];
-            bad |= fir_nonfinite(v.x) | fir_nonfinite(v.y);
-            if (g < n) y[g] = v;
-        }
-    }
-    if (ph_wg) {
-        const unsigned long long p3 = __builtin_amdgcn_s_memtime();
-        unsigned long long *ph = a.phases + 8 * shared_cu;
-        atomicAdd(ph + 0, p1 - p0);
-        atomicAdd(ph + 1, p2 - p1);
-        atomicAdd(ph + 2, p3 - p2);
-        atomicAdd(ph + 3, 1ull);
-    }
-    if (__syncthreads_or(bad)) {
-        const int o0 = 64 * (tid / W) + tid % W;
-#pragma unroll 1
-        for (int q = 0; q < Q; ++q) {
-            const int64_t go = tile0 + o0 + W * q;       // output sample
-            if (go >= n) continue;
-            const int64_t w0 = go - (T - 1);             // its oldest window sample
-            auto xs = [&](int k) -> f2 {
-                const int64_t g = w0 + k;
-                return g < 0 ? hist[T - 1 + g] : x[g];
-            };
-            y[go] = fir_exact_one(xs, hrev, T, W);
-        }
-    }
-#endif
     if (clk_wg) {
         const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = wall_clock64();
         atomicAdd(a.clk, c1 - c0);

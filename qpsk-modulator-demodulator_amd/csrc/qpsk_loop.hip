@@ -56,31 +56,9 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 // sample ring holds 4 rounds (index = p & (4*KB - 1)), preceded by a mirror of
 // its last 4 samples so the 4 interpolation taps are always contiguous in LDS.
 constexpr int kMir = 4;
-#ifndef QPSK_COSTAS_UNROLL2
-#define QPSK_COSTAS_UNROLL2 1
-#endif
-#ifndef QPSK_LOOP_ROTB
-#define QPSK_LOOP_ROTB 1   // decisions-only Costas -> decode slots when no symbols are written
-#endif
-#ifndef QPSK_MM_LSHLADD
-#define QPSK_MM_LSHLADD 1
-#endif
-// Costas wrap as |tn| - 2pi with tn's sign xored in, and -(eq*mi) as a sign
-// flip of mi's high word: 2 VALU fewer per symbol (49 -> 47), bit-exact in the
-// GPU suite, but measured no faster: C3 +0.5 %, C2 -1.1 % (the M&M wave, which
-// paces C2, slows as the Costas wave's LDS reads bunch up), C4 -0.4 %
-// (profiles/r04_costas_wrap_ab.txt); off
-#ifndef QPSK_COSTAS_WRAP_ABS
-#define QPSK_COSTAS_WRAP_ABS 0
-#endif
-
-#ifndef QPSK_RING_PAD
-#define QPSK_RING_PAD 0
-#endif
 template <int KB> struct Ring {
     static constexpr int len = 4 * KB;
-    static constexpr int PAD = QPSK_RING_PAD;
-    static constexpr int row = kMir + len + PAD;   // per-stream LDS row: [mirror 4][ring][pad]
+    static constexpr int row = kMir + len;   // per-stream LDS row: [mirror 4][ring]
 };
 // symbols per round per stream (template CAP): at most floor((KB + 3) / (sps - 0.1)) + 1
 // start in one round: 75 (KB 64, sps >= 1), 36 (KB 64, sps >= 2), 69 (KB 128, sps >= 2)
@@ -95,9 +73,6 @@ constexpr int kCapSps8 = 14;
 // 128-sample rounds at sps >= 8 (variant 4): lag_max = 64 needs
 // (CAP - 1)(sps - 0.1) >= KB + 4 + 64 -> CAP = 26
 constexpr int kCap128Sps8 = 26;
-// 32-sample rounds at sps >= 8 (variant 5, 64 streams: every lane of the
-// stage waves busy): lag_max = 16 needs (CAP - 1)(sps - 0.1) >= 52 -> CAP = 8
-constexpr int kCap32Sps8 = 8;
 // 256-sample rounds at sps >= 8 (variant 6): lag_max = 128 needs
 // (CAP - 1)(sps - 0.1) >= KB + 4 + 128 -> CAP = 51
 constexpr int kCap256Sps8 = 51;
@@ -106,26 +81,12 @@ constexpr int kCap256Sps8 = 51;
 constexpr int kCap512Sps8 = 100;
 typedef double d2 __attribute__((ext_vector_type(2)));
 
-// M&M -> Costas symbol slots: doubles (default; the M&M wave has them widened
-// already) or floats (QPSK_SYM_F32=1: 21 KB less LDS, widened by the Costas
-// wave).  Same results; A/B on one MI355X (C3, serial calls): doubles 45.6 ms,
-// floats 47.6 ms per loop launch, so the smaller footprint -- which would let
-// one matched-filter workgroup of the next pipelined call share the CU -- does
-// not pay for the two extra conversions on the Costas wave
-#ifndef QPSK_SYM_F32
-#define QPSK_SYM_F32 0
-#endif
-#if QPSK_SYM_F32
-typedef f2 sym_t;
-__device__ __forceinline__ sym_t to_sym(float ci, float cq, double, double) { return f2{ci, cq}; }
-__device__ __forceinline__ d2 from_sym(f2 v) { return d2{static_cast<double>(v.x), static_cast<double>(v.y)}; }
-__device__ __forceinline__ f2 sym_to_f2(f2 v) { return v; }
-#else
+// M&M -> Costas symbol slots hold doubles: the M&M wave has them widened
+// already.  Float slots (21 KB less LDS) measured slower, the two widenings
+// landing on the Costas wave (C3 loop 45.6 vs 47.6 ms, round 2)
 typedef d2 sym_t;
 __device__ __forceinline__ sym_t to_sym(float, float, double cid, double cqd) { return d2{cid, cqd}; }
 __device__ __forceinline__ d2 from_sym(d2 v) { return v; }
-__device__ __forceinline__ f2 sym_to_f2(d2 v) { return f2{static_cast<float>(v.x), static_cast<float>(v.y)}; }
-#endif
 
 __device__ __forceinline__ int wave_max_i32(int v) {
 #pragma unroll
@@ -202,7 +163,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     constexpr int kRing = Ring<KB>::len, kRowS = Ring<KB>::row;
     // one LDS object only: a second __shared__ object would make hipcc drain the
     // loader's LDS-DMA before touching it (cdna_hip_programming.md §5)
-    constexpr bool ROTB = QPSK_LOOP_ROTB && !SYMS;
+    constexpr bool ROTB = !SYMS;
     __shared__ LoopLds<SPW, CAP, KB, TRIG, ROTB> L;
 
     const int wave = threadIdx.x >> 6;
@@ -217,14 +178,16 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     // vmcnt waits count its own outstanding memory operations)
     KtEnd kte{wave != 0 ? a.kt : nullptr};
     ClkSample clk{wave == 1 && lane == 0 ? a.clk : nullptr};
-    // FIR phase sample: this workgroup's CU is marked while its M&M wave runs
+    // FIR phase sample: this workgroup's CU is counted while its M&M wave runs
+    // (a count, not a flag: two loop workgroups may share a CU, and the first
+    // to leave must not clear the other's mark)
     struct CuMark {
         unsigned *p;
         __device__ explicit CuMark(unsigned *map) : p(map ? map + cu_key() : nullptr) {
-            if (p) __hip_atomic_store(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (p) __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __device__ ~CuMark() {
-            if (p) __hip_atomic_store(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (p) __hip_atomic_fetch_sub(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     } cu_mark{wave == 1 && lane == 0 ? a.cu_map : nullptr};
     // the batch spread evenly over the grid: workgroup b owns streams
@@ -306,9 +269,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         }
         cmin = __builtin_amdgcn_readfirstlane(cmin);
         auto issue = [&](int r) {
-#ifdef QPSK_PROBE_NOLOAD
-            return;   // diagnostic: no LDS DMA (the consumers read stale samples)
-#endif
             const int roff = (r & 3) * KB;
             if ((r + 1) * KB <= cmin) {
                 const char *rb = reinterpret_cast<const char *>(wg_mf + static_cast<int64_t>(r) * KB);
@@ -366,20 +326,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         return;
     }
 
-#ifdef QPSK_PROBE_NOMM
-    if (wave == 1) {   // diagnostic: a stand-in M&M that only feeds 8 fixed symbols a round
-        for (int r = 0; r <= NR + 1; ++r) {
-            __builtin_amdgcn_s_barrier();
-            if (r >= NR) continue;
-            sym_t *out = L.sym + ((r & 1) * SPW + lane) * L.RS;
-            if (lane < SPW)
-                for (int k = 0; k < 8; ++k) out[k] = to_sym(0.7f, -0.7f, 0.7 + 0.01 * k, -0.7 + 0.02 * k);
-            if (lane < SPW) L.cnt[(r & 3) * SPW + lane] = mine ? 8 : 0;
-            if (lane == 0) L.cnt[4 * SPW + (r & 3)] = 8;
-        }
-        return;
-    }
-#endif
     if (wave == 1) {
         // ============================================================ M&M
         StreamState st;
@@ -413,15 +359,11 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         auto taps_fl = [&](double fl) -> lds_f2 * {
             union { double v; unsigned long long u; } kb;
             kb.v = fl + tap_shift;
-#if QPSK_MM_LSHLADD
             // and + lshl_add: one op shorter than the shift, and, add the
             // compiler canonicalises 8 * (i & m) + base into
             const uint32_t idx = static_cast<uint32_t>(kb.u) & (kRing - 1);
             uint32_t addr;
             asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(addr) : "v"(idx), "v"(tap0));
-#else
-            const uint32_t addr = tap0 + 8u * (static_cast<uint32_t>(kb.u) & (kRing - 1));
-#endif
             return reinterpret_cast<lds_f2 *>(static_cast<uintptr_t>(addr));
         };
         // symbols that start in every 64-sample round once a stream is inside its
@@ -681,21 +623,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         return;
     }
 
-#ifdef QPSK_PROBE_NOCOSTAS
-    if (wave == 2) {   // diagnostic: a stand-in Costas that copies symbols through
-        for (int r = 0; r <= NR + 1; ++r) {
-            __builtin_amdgcn_s_barrier();
-            if (r == 0 || r > NR || lane >= SPW) continue;
-            const int slot = (r - 1) & 1;
-            const int m = mine ? L.cnt[((r - 1) & 3) * SPW + lane] : 0;
-            for (int k = 0; k < m; ++k) {
-                if constexpr (ROTB) L.rot[(slot * SPW + lane) * L.RS + k] = 0;
-                else L.rot[(slot * SPW + lane) * L.RS + k] = sym_to_f2(L.sym[(slot * SPW + lane) * L.RS + k]);
-            }
-        }
-        return;
-    }
-#endif
     if (wave == 2) {
         // ============================================================ Costas
         // TRIG 1: lanes l and l + 32 both run stream l (SPW <= 32), for the split
@@ -786,39 +713,13 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 // rounds the same exact difference as the reference's subtraction
                 const double ei = ri >= 0.0f ? 1.0 : -1.0;
                 const double eq = rq >= 0.0f ? 1.0 : -1.0;
-#if QPSK_COSTAS_WRAP_ABS
-                // -(eq*mi) = mi with its sign bit flipped unless eq = -1: one
-                // v_bitop3 on mi's high word (mi is dead after it, so the pair
-                // stays in place) instead of a multiply by a +-1.0 pair built
-                // around a copied zero word
-                const uint64_t mib = __builtin_bit_cast(uint64_t, mi);
-                const uint32_t eqhw = static_cast<uint32_t>(__builtin_bit_cast(uint64_t, eq) >> 32);
-                const uint32_t nmh = static_cast<uint32_t>(mib >> 32) ^ (~eqhw & sgn_v);
-                const double pe = fma(ei, mq, __builtin_bit_cast(double, (static_cast<uint64_t>(nmh) << 32) |
-                                                                             static_cast<uint32_t>(mib)));
-#else
                 const double pe = fma(ei, mq, -(eq * mi));
-#endif
                 freq = freq + cb * pe;
                 const double tn = theta + (freq + ca * pe);
-#if QPSK_COSTAS_WRAP_ABS
-                // single +-2pi wrap (:89-91) as a select: above pi tn - 2pi =
-                // |tn| - 2pi, below -pi tn + 2pi = -(|tn| - 2pi) (rounding is
-                // sign-symmetric), so the wrapped value is |tn| - 2pi (one add
-                // with an abs modifier) with tn's sign bit xored into its high
-                // word (one v_bitop3); the select takes the halves separately,
-                // so no register pair has to be assembled
-                const double am = fabs(tn) - kTwoPi;
-                const uint64_t tnb = __builtin_bit_cast(uint64_t, tn), amb = __builtin_bit_cast(uint64_t, am);
-                const uint32_t twh = static_cast<uint32_t>(amb >> 32) ^ (static_cast<uint32_t>(tnb >> 32) & sgn_v);
-                const double tw = __builtin_bit_cast(double, (static_cast<uint64_t>(twh) << 32) | static_cast<uint32_t>(amb));
-                theta = fabs(tn) > kPi ? tw : tn;
-#else
                 // single +-2pi wrap (:89-91) as a select: tn - copysign(2pi, tn)
                 // is tn - 2pi above pi and tn + 2pi below -pi
                 const double tw = tn - copysign(kTwoPi, tn);
                 theta = fabs(tn) > kPi ? tw : tn;
-#endif
                 if constexpr (ROTB) {
                     // the decisions' sign bytes (byte 3 of the high words of +-1.0)
                     const uint32_t eih = static_cast<uint32_t>(__builtin_bit_cast(uint64_t, ei) >> 32);
@@ -837,7 +738,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             if (m >= mlo) {              // every stream the M&M ran uniformly
                 // one v_max_f64 (fmax would first canonicalize amax)
                 auto track = [&]() { asm volatile("v_max_f64 %0, %0, |%1|" : "+v"(amax) : "v"(theta)); };
-#if QPSK_COSTAS_UNROLL2
                 // by two: y and the next symbol alternate registers instead of
                 // being copied back every symbol
                 for (; k + 1 < mlo; k += 2) {   // uniform trip count
@@ -851,13 +751,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                     track();
                     ++k;
                 }
-#else
-#pragma unroll 4
-                for (; k < mlo; ++k) {   // uniform trip count
-                    step(k, std::false_type{});
-                    track();
-                }
-#endif
             }
             ACC(k_uni, tu);
 #ifdef QPSK_LOOP_STAMPS
@@ -895,10 +788,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
     }
 
     // ================================================================ decode
-#ifdef QPSK_PROBE_NODECODE
-    for (int r = 0; r <= NR + 1; ++r) __builtin_amdgcn_s_barrier();   // diagnostic
-    return;
-#endif
     // the decode wave runs the real lanes only (its per-lane loop is off the chains)
     const bool dmine = real && mine;
     int diff_have = 0;
@@ -1010,12 +899,8 @@ static int launch_loop_spw_t(const LoopArgs &a, const LoopParams &P, int mode, h
 
 template <int SPW, int CAP, int KB, int ACT = SPW>
 static int launch_loop_spw(const LoopArgs &a, const LoopParams &P, int mode, hipStream_t stream) {
-    if constexpr (ACT > 32) {   // the split glibc sincos needs both wave halves per stream
-        return launch_loop_spw_t<SPW, CAP, KB, 0, ACT>(a, P, mode, stream);
-    } else {
-        return P.costas_trig ? launch_loop_spw_t<SPW, CAP, KB, 1, ACT>(a, P, mode, stream)
-                             : launch_loop_spw_t<SPW, CAP, KB, 0, ACT>(a, P, mode, stream);
-    }
+    return P.costas_trig ? launch_loop_spw_t<SPW, CAP, KB, 1, ACT>(a, P, mode, stream)
+                         : launch_loop_spw_t<SPW, CAP, KB, 0, ACT>(a, P, mode, stream);
 }
 
 int launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant, hipStream_t stream) {
@@ -1034,11 +919,6 @@ int launch_loop(const LoopArgs &a, const LoopParams &P, int mode, int variant, h
         return launch_loop_spw<16, kCap128Sps2, 128>(a, P, mode, stream);
     else if (variant == 4 && P.sps >= 8.0)
         return launch_loop_spw<24, kCap128Sps8, 128>(a, P, mode, stream);
-    else if (variant == 5 && P.sps >= 8.0 && !P.costas_trig)
-        // 64 streams x 32-sample rounds: every stage-wave lane busy, 105 KB of
-        // LDS (a 4-round ring of 64-sample rounds for 64 streams would take
-        // 133 KB alone); measured, not the default
-        return launch_loop_spw<64, kCap32Sps8, 32>(a, P, mode, stream);
     else if (variant == 6 && P.sps >= 8.0)
         // 12 streams x 256-sample rounds, 32 busy lanes (20 shadow lanes on
         // row 0): a quarter of the rounds of 32 x 64, 135 KB of LDS

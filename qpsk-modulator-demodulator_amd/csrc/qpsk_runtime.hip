@@ -739,8 +739,17 @@ int qpsk_demod_enable_fir_phases(qpsk_demod *h, int32_t on) {
     if ((rc = drain_async(h))) return rc;
     HIP_TRY(hipSetDevice(h->p.device));
     HIP_TRY(hipStreamSynchronize(h->stream));
-    if (on && !h->d_phases) {
-        if ((rc = dev_alloc(&h->d_phases, kFirPhaseWords)) || (rc = dev_alloc(&h->d_cu_map, kCuKeys))) return rc;
+    if (on && (!h->d_phases || !h->d_cu_map)) {
+        // both or neither: a half-allocated pair would let the sampled FIR
+        // workgroups read a null cu_map
+        if ((!h->d_phases && (rc = dev_alloc(&h->d_phases, kFirPhaseWords))) ||
+            (!h->d_cu_map && (rc = dev_alloc(&h->d_cu_map, kCuKeys)))) {
+            hipFree(h->d_phases);
+            hipFree(h->d_cu_map);
+            h->d_phases = nullptr;
+            h->d_cu_map = nullptr;
+            return rc;
+        }
         HIP_TRY(hipMemset(h->d_cu_map, 0, kCuKeys * sizeof(unsigned)));
     }
     if (on) HIP_TRY(hipMemset(h->d_phases, 0, kFirPhaseWords * sizeof(unsigned long long)));
@@ -1348,7 +1357,6 @@ int32_t qpsk_demod_pick_loop_variant(int32_t requested, int32_t n_streams, doubl
     const int64_t S = n_streams;
     if ((S + 5) / 6 <= cus) return 7;
     if ((S + 11) / 12 <= cus) return 6;
-    if ((S + 23) / 24 <= cus / 2) return 4;
     return 0;
 }
 

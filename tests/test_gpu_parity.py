@@ -47,7 +47,9 @@ def oracle_run(iq2d, calls, sps, span, mode=None, **kw):
     return out
 
 
-def gpu_run(iq2d, calls, sps, span, mode=None, **kw):
+def gpu_run(iq2d, calls, sps, span, mode=None, want_syms=True, **kw):
+    """want_syms=False runs the bits-only kernel (decisions-only Costas ->
+    decode slots); its rows carry bits and None for the symbols."""
     S = iq2d.shape[0]
     p = Q.params(K.FS, K.FS // sps, K.ALPHA, span, max_samples_per_call=max(max(c) for c in calls) + 8, **kw)
     b = Q.BatchDemodulator(S, p)
@@ -61,11 +63,11 @@ def gpu_run(iq2d, calls, sps, span, mode=None, **kw):
             x[s, : 2 * lens[s]] = iq2d[s, 2 * pos[s]: 2 * (pos[s] + lens[s])]
         uniform = all(l == lens[0] for l in lens)
         bits, nb, syms, ns = b.process(x[:, : 2 * n] if n else x[:, :0], mode=m,
-                                       lengths=None if uniform else np.array(lens), want_syms=True)
+                                       lengths=None if uniform else np.array(lens), want_syms=want_syms)
         res = []
         for s in range(S):
             bs = Q.unpack_bits(bits[s], int(nb[s])) if m == Q.MODE_DEMODULATE else ""
-            res.append((bs, syms[s, : 2 * int(ns[s])].copy()))
+            res.append((bs, syms[s, : 2 * int(ns[s])].copy() if want_syms else None))
         pos += np.array(lens)
         out.append(res)
     b.close()
@@ -76,6 +78,8 @@ def assert_same(a, b, exact=True):
     for ci, (ra, rb) in enumerate(zip(a, b)):
         for s, ((ba, sa), (bb, sb)) in enumerate(zip(ra, rb)):
             assert ba == bb, f"call {ci} stream {s}: bits differ ({len(ba)} vs {len(bb)})"
+            if sa is None or sb is None:
+                continue
             assert sa.shape == sb.shape, f"call {ci} stream {s}: symbol count"
             if exact:
                 assert np.array_equal(sa, sb), f"call {ci} stream {s}: symbols differ"
@@ -91,13 +95,13 @@ def test_single_call_bit_exact(sps, span):
 
 
 @pytest.mark.parametrize("sps,span", K.CONFIGS)
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 6, 7])
 def test_chunked_ragged_calls_bit_exact(sps, span, variant):
     """Every loop-kernel shape (qpsk_demod_params.loop_variant) on ragged calls,
     including 0/1/2/3-sample calls and calls longer than a round."""
     if variant == 3 and sps < 2:
         pytest.skip("16 x 128 needs sps >= 2 (the launcher never picks it below)")
-    if variant in (4, 5, 6, 7) and sps < 8:
+    if variant in (4, 6, 7) and sps < 8:
         pytest.skip("24 x 128, 64 x 32 and 12 x 256 are sps >= 8 shapes (below it the launcher falls back to auto)")
     iq = K.batch_signals(4, seed0=20, sps=sps, span=span, n_bits=2400, snr_db=14)
     n = iq.shape[1] // 2
@@ -111,7 +115,10 @@ def test_chunked_ragged_calls_bit_exact(sps, span, variant):
         calls.append(c)
         left -= np.array(c)
         k += 1
-    assert_same(gpu_run(iq, calls, sps, span, loop_variant=variant), oracle_run(iq, calls, sps, span))
+    ref = oracle_run(iq, calls, sps, span)
+    assert_same(gpu_run(iq, calls, sps, span, loop_variant=variant), ref)
+    # the production bits-only kernel on the same ragged calls
+    assert_same(gpu_run(iq, calls, sps, span, loop_variant=variant, want_syms=False), ref)
 
 
 @pytest.mark.parametrize("variant", [4, 6, 7])
@@ -129,7 +136,9 @@ def test_long_round_shapes_many_streams_bit_exact(variant):
         calls.append([int(v) for v in lens])
         used += lens
     calls.append([int(n - u) for u in used])
-    assert_same(gpu_run(iq, calls, sps, span, loop_variant=variant), oracle_run(iq, calls, sps, span))
+    ref = oracle_run(iq, calls, sps, span)
+    assert_same(gpu_run(iq, calls, sps, span, loop_variant=variant), ref)
+    assert_same(gpu_run(iq, calls, sps, span, loop_variant=variant, want_syms=False), ref)
 
 
 @pytest.mark.parametrize("sps,span", [(30, 6), (100, 4), (200, 2), (300, 2), (1000, 1)])

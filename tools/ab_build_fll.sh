@@ -2,7 +2,7 @@
 # tools/ab_build_fll.sh NAME [SRC] [hipcc flags...] -- an A/B variant of the FLL:
 # qpsk-modulator-demodulator_amd/_build/ab/libNAME.so = the in-tree library with
 # qpsk_fll.o rebuilt from SRC (default csrc/qpsk_fll.hip) under the extra flags
-# (e.g. -DQPSK_FLL_PROBE=16).  Run `make -C qpsk-modulator-demodulator_amd` first.
+# (e.g. -DNAME=VALUE for an A/B macro).  Run `make -C qpsk-modulator-demodulator_amd` first.
 set -e
 name=$1; shift
 root=$(cd "$(dirname "$0")/.." && pwd)
