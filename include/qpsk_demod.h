@@ -162,18 +162,23 @@ int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t str
  *  - bits / n_bits / syms / n_syms are complete after qpsk_demod_pipeline_wait.
  *  - synchronous process(), get/set_state, set_stream and destroy first wait
  *    for every pipelined call.
- *  - Residency gate: call k+1's matched filter waits ON THE DEVICE
- *    (hipStreamWaitValue64, no timeout) until call k's symbol-loop workgroups
- *    hold their CUs, so the two always overlap in the same order.  Under
+ *  - Residency gate: call k+1's matched filter waits ON THE DEVICE (a
+ *    one-wave kernel ahead of it on the front stream) until call k's
+ *    symbol-loop workgroups hold their CUs, so the two always overlap in the
+ *    same order.  The wait is bounded: after QPSK_GATE_TIMEOUT_MS (default
+ *    2000 ms, read at create) the filter goes ahead and the timeout is counted
+ *    (qpsk_demod_gate_timeouts); results never depend on the gate.  Under
  *    serialised dispatch the loop kernel could only start after the waiting
- *    filter, so the gate is off when qpsk_pipeline_gate_enabled() says so:
+ *    filter, so every wait would run out: the gate is off when
+ *    qpsk_pipeline_gate_enabled() says so:
  *    QPSK_PIPELINE_GATE=0, AMD_SERIALIZE_KERNEL or AMD_SERIALIZE_COPY != 0,
  *    HIP_LAUNCH_BLOCKING or CUDA_LAUNCH_BLOCKING != 0, rocprofv3 counter
  *    collection (ROCPROF_COUNTER_COLLECTION=1) or kernel serialisation
  *    (ROCPROFILER_KERNEL_SERIALIZATION), HSA_ENABLE_DEBUG.  A tool that
  *    serialises dispatch without any of these (e.g. a debugger attached after
- *    start-up) can stall process_async: set QPSK_PIPELINE_GATE=0 for such runs
- *    (results are identical with the gate off; only the overlap order may vary).
+ *    start-up) costs one timeout per call: set QPSK_PIPELINE_GATE=0 for such
+ *    runs (results are identical with the gate off; only the overlap order may
+ *    vary).
  *    QPSK_PIPELINE_GATE=1 forces it on.  Read once per handle, at create.
  */
 int qpsk_demod_process_async(qpsk_demod *h, int32_t mode, const float *iq, int64_t stride_floats,
@@ -183,6 +188,9 @@ int qpsk_demod_process_async(qpsk_demod *h, int32_t mode, const float *iq, int64
 /* 1 if handles created now use the residency gate, 0 if the environment turns
  * it off (the list above); needs no device. */
 int qpsk_pipeline_gate_enabled(void);
+/* Residency-gate waits of this handle that ran out (QPSK_GATE_TIMEOUT_MS) since
+ * it was created, after every queued call; 0 in normal operation. */
+int qpsk_demod_gate_timeouts(qpsk_demod *h, uint64_t *count);
 /* The symbol-loop shape qpsk_demod_create picks for loop_variant = 0 (auto):
  * at sps >= 8, 7 (6 streams x 512-sample rounds) while ceil(S/6) <= cus, else
  * 6 (12 x 256) while ceil(S/12) <= cus, else 0 (the launcher's default for the

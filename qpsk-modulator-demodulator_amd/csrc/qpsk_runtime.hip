@@ -186,9 +186,16 @@ struct qpsk_demod {
     uint64_t resident_gate = 0;      // what the newest gated loop launch brings it to, at least
     bool gate_pending = false;       // the next FIR has a loop launch to wait for
     // off under a profiler's counter collection (rocprofv3 --pmc serialises
-    // every dispatch, and a stream parked on the wait then stalls the loop
-    // kernel it waits for) or with QPSK_PIPELINE_GATE=0
+    // every dispatch, so the wait would run to its cap on every call) or with
+    // QPSK_PIPELINE_GATE=0
     bool use_gate = true;
+    // the wait is bounded (gate_wait_kernel): at most gate_cap_ticks of the
+    // wall clock (QPSK_GATE_TIMEOUT_MS, default 2000 ms), counted in d_gate[0]
+    // when it runs out; gate_publish = false (QPSK_GATE_NO_PUBLISH=1, tests
+    // only) keeps the loop workgroups from counting, so every wait runs out
+    unsigned *d_gate = nullptr;
+    unsigned long long gate_cap_ticks = 0;
+    bool gate_publish = true;
     int last_back = -1;              // boundary buffer of the newest back stage, -1 = none
     int64_t *h_len[2] = {nullptr, nullptr};   // pinned staging of per-call lengths
     // FLL on: the back stage (loop kernel) of the newest call is issued by the
@@ -327,6 +334,37 @@ int run_fir(qpsk_demod *h, const float *x, int64_t x_stride, const int64_t *d_le
     return QPSK_OK;
 }
 
+// The residency gate of the pipelined path (process_async_one): one wave on
+// the front stream, ahead of the FIR, polls the counter the loop kernel's
+// workgroups bump as they start (s_sleep between reads) and ends when it
+// reaches target -- or when cap wall-clock ticks have passed, counted in
+// *timeouts.  The FIR behind it in stream order is dispatched only then, as
+// with hipStreamWaitValue64, but a counter that never arrives (a dispatch
+// serialised by a tool the environment predicate does not know) costs one cap
+// per call instead of a hang.  The gate orders dispatch only; no result
+// depends on it.
+__global__ void gate_wait_kernel(const unsigned long long *resident, unsigned long long target,
+                                 unsigned long long cap, unsigned *timeouts) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(resident, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+        if (wall_clock64() - t0 > cap) {
+            atomicAdd(timeouts, 1u);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+
+int gate_wait(qpsk_demod *h, hipStream_t st) {
+    if (!h->gate_pending) return QPSK_OK;
+    h->gate_pending = false;
+    hipLaunchKernelGGL(gate_wait_kernel, dim3(1), dim3(64), 0, st, h->d_resident,
+                       static_cast<unsigned long long>(h->resident_gate), h->gate_cap_ticks, h->d_gate);
+    HIP_TRY(hipGetLastError());
+    return QPSK_OK;
+}
+
 // symbol sync + Costas + decode (QPSKDeModulator.cs:364-408) and the output copies
 // resident: the pipelined path's residency counter (nullptr otherwise); the
 // launch's workgroup count is added to h->resident_issued
@@ -378,7 +416,7 @@ int run_loop(qpsk_demod *h, const Call &c, const int64_t *d_len, float *mf, hipS
     la.kt = kt ? kt + 4 : nullptr;
     la.clk = kt ? kt + 10 : nullptr;
     la.cu_map = h->fir_phases ? h->d_cu_map : nullptr;
-    la.resident = resident;
+    la.resident = h->gate_publish ? resident : nullptr;
     const int grid = launch_loop(la, h->lp, c.mode, h->loop_variant, st);
     HIP_TRY(hipGetLastError());
     if (resident) {
@@ -461,6 +499,8 @@ int pipe_setup(qpsk_demod *h) {
                                   hipMallocSignalMemory));
     HIP_TRY(hipMemset(h->d_resident, 0, sizeof(unsigned long long)));
     int rc;
+    if ((rc = dev_alloc(&h->d_gate, 1))) return rc;
+    HIP_TRY(hipMemset(h->d_gate, 0, sizeof(unsigned)));
     if (!h->d_lengths[1] && (rc = dev_alloc(&h->d_lengths[1], h->S))) return rc;
     // the second boundary buffer: MF rows (the FIR of one call writes one while
     // the loop kernel of the previous call reads the other).  No room for it
@@ -609,6 +649,13 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
     // half-empty waves cost the FIR beside them issue slots
     h->loop_variant = qpsk_demod_pick_loop_variant(h->loop_variant, h->S, h->lp.sps, h->cus);
     h->use_gate = qpsk_pipeline_gate_enabled() == 1;
+    {
+        const char *v = std::getenv("QPSK_GATE_TIMEOUT_MS");
+        const long ms = v && *v ? std::strtol(v, nullptr, 10) : 2000;
+        h->gate_cap_ticks = static_cast<unsigned long long>(ms > 0 ? ms : 1) * static_cast<unsigned>(h->wall_khz);
+        const char *np = std::getenv("QPSK_GATE_NO_PUBLISH");
+        h->gate_publish = !(np && *np && std::strcmp(np, "0") != 0);
+    }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipStreamCreate failed"));
     h->own_stream = true;
@@ -672,6 +719,7 @@ int qpsk_demod_destroy(qpsk_demod *h) {
         if (h->e_back[b]) hipEventDestroy(h->e_back[b]);
     }
     if (h->d_resident) hipFree(h->d_resident);
+    hipFree(h->d_gate);
     hipFree(h->d_kt);
     hipFree(h->d_phases);
     hipFree(h->d_cu_map);
@@ -968,9 +1016,7 @@ int process_async_one(qpsk_demod *h, const Call &c) {
             h->back_rec[db] = true;
             h->last_back = db;
         }
-        if (h->gate_pending)
-            HIP_TRY(hipStreamWaitValue64(F, h->d_resident, h->resident_gate, hipStreamWaitValueGte));
-        h->gate_pending = false;
+        if ((rc = gate_wait(h, F))) return rc;
         mf = h->d_mf[b];
         if ((rc = run_fir(h, n_call > 0 ? h->d_fll_out[0] : x, n_call > 0 ? h->n_max : x_stride, d_len, n_call,
                           mf, F, kt)))
@@ -996,12 +1042,10 @@ int process_async_one(qpsk_demod *h, const Call &c) {
         // call.  So FIR(k+1) waits, on the device, until loop(k)'s workgroups
         // hold their CUs: each adds 1 to the residency counter as it starts,
         // and the front stream waits for the count (hipStreamWaitValue64 on
-        // signal memory).  The order no longer depends on dispatch timing:
-        // the FIR cannot be dispatched before min(grid, CUs) loop workgroups
-        // run, and every one of those was dispatched before it.
-        if (h->gate_pending)
-            HIP_TRY(hipStreamWaitValue64(F, h->d_resident, h->resident_gate, hipStreamWaitValueGte));
-        h->gate_pending = false;
+        // signal memory, gate_wait: bounded).  The order no longer depends on
+        // dispatch timing: the FIR cannot be dispatched before min(grid, CUs)
+        // loop workgroups run, and every one of those was dispatched before it.
+        if ((rc = gate_wait(h, F))) return rc;
         mf = h->d_mf[b];
         if ((rc = run_fir(h, x, x_stride, d_len, n_call, mf, F, kt))) return rc;
         HIP_TRY(hipEventRecord(h->e_front[b], F));
@@ -1219,6 +1263,19 @@ int qpsk_demod_pipeline_wait(qpsk_demod *h, void *hip_stream) {
     return QPSK_OK;
 }
 
+int qpsk_demod_gate_timeouts(qpsk_demod *h, uint64_t *count) {
+    if (!h || !count) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
+    *count = 0;
+    if (!h->d_gate) return QPSK_OK;
+    int rc;
+    if ((rc = drain_async(h))) return rc;
+    HIP_TRY(hipSetDevice(h->p.device));
+    unsigned v = 0;
+    HIP_TRY(hipMemcpy(&v, h->d_gate, sizeof(unsigned), hipMemcpyDeviceToHost));
+    *count = v;
+    return QPSK_OK;
+}
+
 int qpsk_demod_pipeline_depth(const qpsk_demod *h) {
     if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
     return h->pipe_ready ? h->pipe_bufs : 0;
@@ -1360,9 +1417,10 @@ int32_t qpsk_demod_pick_loop_variant(int32_t requested, int32_t n_streams, doubl
     return 0;
 }
 
-// Residency gate default (process_async_one).  hipStreamWaitValue64 cannot
-// time out, so the gate is off wherever dispatch may be serialised and the
-// loop kernel it waits for would only start after the waiting FIR.
+// Residency gate default (process_async_one).  The wait is bounded
+// (gate_wait_kernel), but where dispatch is serialised the loop kernel it
+// waits for starts only after the waiting FIR, so every wait would run to its
+// cap: the gate is off there.
 int qpsk_pipeline_gate_enabled(void) {
     auto env = [](const char *name) -> const char * {
         const char *v = std::getenv(name);

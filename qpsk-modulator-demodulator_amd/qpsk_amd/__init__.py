@@ -180,6 +180,7 @@ def lib():
     L.qpsk_demod_get_state.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     L.qpsk_demod_set_state.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     L.qpsk_pipeline_gate_enabled.restype = C.c_int
+    L.qpsk_demod_gate_timeouts.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     L.qpsk_demod_pick_loop_variant.argtypes = [C.c_int32, C.c_int32, C.c_double, C.c_int32]
     L.qpsk_demod_pick_loop_variant.restype = C.c_int32
     L.qpsk_demod_enable_fir_phases.argtypes = [C.c_void_p, C.c_int32]
@@ -221,7 +222,8 @@ EXPORTED_SYMBOLS = [
     "qpsk_demod_kernel_clocks",
     "qpsk_demod_rrc_taps",
     "qpsk_demod_gains", "qpsk_demod_fll_taps", "qpsk_demod_state_bytes", "qpsk_demod_get_state",
-    "qpsk_demod_set_state", "qpsk_pipeline_gate_enabled", "qpsk_demod_pick_loop_variant",
+    "qpsk_demod_set_state", "qpsk_pipeline_gate_enabled", "qpsk_demod_gate_timeouts",
+    "qpsk_demod_pick_loop_variant",
     "qpsk_demod_enable_fir_phases",
     "qpsk_demod_fir_phases", "qpsk_demod_design", "qpsk_framer_create", "qpsk_framer_destroy",
     "qpsk_framer_set_markers", "qpsk_framer_push", "qpsk_framer_dev_create",
@@ -503,6 +505,12 @@ class BatchDemodulator:
 
     def pipeline_depth(self) -> int:
         return _check(lib().qpsk_demod_pipeline_depth(self._h))
+
+    def gate_timeouts(self) -> int:
+        """Residency-gate waits that ran out (QPSK_GATE_TIMEOUT_MS) so far."""
+        v = C.c_uint64()
+        _check(lib().qpsk_demod_gate_timeouts(self._h, C.byref(v)))
+        return v.value
 
 
 class HostRing:

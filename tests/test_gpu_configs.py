@@ -127,9 +127,10 @@ def test_baseline_workload_seven_calls_vs_libm_oracle(key, trig):
                     assert np.max(np.abs(g - rsy), initial=0) <= SYM_TOL, f"{key} stream {s} call {k}"
 
 
-def _pipelined_rows(S, n, calls, sps, span, seed, idx, **kw):
+def _pipelined_rows(S, n, calls, sps, span, seed, idx, stats=None, **kw):
     """`calls` consecutive pipelined calls of n samples on a GPU-synthesised
-    batch; returns the host input rows idx and per call (bits, n_bits) of idx."""
+    batch; returns the host input rows idx and per call (bits, n_bits) of idx
+    (stats: a dict that receives the handle's gate timeouts)."""
     import torch
     dev = torch.device("cuda", 0)
     iq, _ = Q.synth_generate(S, n * calls, K.FS, K.FS // sps, rrc_alpha=K.ALPHA, rrc_span=span, seed=seed,
@@ -150,6 +151,8 @@ def _pipelined_rows(S, n, calls, sps, span, seed, idx, **kw):
     torch.cuda.synchronize(dev)
     host = _rows(iq, idx)
     got = [(_rows(bits, idx), _rows(nb, idx)) for _, bits, nb in outs]
+    if stats is not None:
+        stats["gate_timeouts"] = b.gate_timeouts()
     b.close()
     return host, got
 
@@ -187,6 +190,32 @@ def test_pipelined_results_do_not_depend_on_the_gate(monkeypatch):
         for s in range(S):
             nb = int(with_gate[k][1][s])
             assert np.array_equal(with_gate[k][0][s][: (nb + 7) // 8], without[k][0][s][: (nb + 7) // 8])
+
+
+def test_gate_that_never_opens_times_out_bit_exact(monkeypatch):
+    """The residency gate's wait is bounded: with the loop kernel's residency
+    count suppressed (QPSK_GATE_NO_PUBLISH=1) every wait runs to its cap
+    (QPSK_GATE_TIMEOUT_MS) and the matched filter goes ahead; the calls still
+    finish, each wait is counted, and the bits are the gated run's."""
+    import time
+    S, n, calls = 300, 8192, 4
+    idx = list(range(S))
+    st = {}
+    _, with_gate = _pipelined_rows(S, n, calls, 8, 8, 0x52, idx, stats=st)
+    assert st["gate_timeouts"] == 0
+    monkeypatch.setenv("QPSK_PIPELINE_GATE", "1")
+    monkeypatch.setenv("QPSK_GATE_NO_PUBLISH", "1")
+    monkeypatch.setenv("QPSK_GATE_TIMEOUT_MS", "200")
+    t0 = time.perf_counter()
+    _, stuck = _pipelined_rows(S, n, calls, 8, 8, 0x52, idx, stats=st)
+    dt = time.perf_counter() - t0
+    assert st["gate_timeouts"] == calls - 1      # every call after the first waited
+    assert dt < 30.0
+    for k in range(calls):
+        assert np.array_equal(with_gate[k][1], stuck[k][1])
+        for s in range(S):
+            nb = int(with_gate[k][1][s])
+            assert np.array_equal(with_gate[k][0][s][: (nb + 7) // 8], stuck[k][0][s][: (nb + 7) // 8])
 
 
 def test_two_pipelined_handles_interleaved():

@@ -11,7 +11,7 @@ for i in $(seq 1 "$rounds"); do
     echo "$(basename "$lib") $(echo "$out" | python3 -c '
 import json, sys
 d = json.loads(sys.stdin.read())
-r = d["rooflines"]
+r = d["kernels"]
 ms = {k: round(v["ms"], 2) for k, v in r.items() if isinstance(v, dict) and "ms" in v}
 lp = r.get("loop", {})
 print(ms, "loop cyc/sym", lp.get("cycles_per_symbol"), "GHz", lp.get("clock_ghz_median"), "value", d["value"])')"
