@@ -514,14 +514,22 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 ACC(c_pre, tl);
                 STAMP(tu);
                 if (live) {
-                    // by two: the loop-carried symbol/decision registers alternate
-                    // instead of being copied back every symbol
+                    // an even unroll: the loop-carried symbol/decision registers
+                    // alternate instead of being copied back every symbol
                     int u = 0;
-                    for (; u + 2 < kg; u += 2) {
+                    // by four: a lone wave pays ~28 cycles per taken loop branch
+                    // (tools/dep_probe.hip), 7 per symbol instead of 14.  C2 loop
+                    // 18.4 -> 17.3 ms (326 -> 306 cycles per symbol, A/B x2 on one
+                    // MI355X, profiles/r05_loop_unroll4_ab.txt); C3 / C4 unchanged
+                    for (; u + 4 < kg; u += 4) {
+                        step(std::true_type{});
+                        step(std::true_type{});
                         step(std::true_type{});
                         step(std::true_type{});
                     }
-                    if (kg - u == 2) step(std::true_type{});
+                    if (kg - u >= 4) step(std::true_type{});
+                    if (kg - u >= 3) step(std::true_type{});
+                    if (kg - u >= 2) step(std::true_type{});
                     if (kg - u >= 1) step(std::false_type{});
                 }
                 ACC(c_uni, tu);
@@ -738,13 +746,25 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             if (m >= mlo) {              // every stream the M&M ran uniformly
                 // one v_max_f64 (fmax would first canonicalize amax)
                 auto track = [&]() { asm volatile("v_max_f64 %0, %0, |%1|" : "+v"(amax) : "v"(theta)); };
-                // by two: y and the next symbol alternate registers instead of
-                // being copied back every symbol
-                for (; k + 1 < mlo; k += 2) {   // uniform trip count
+                // an even unroll: y and the next symbol alternate registers
+                // instead of being copied back every symbol
+                // by four (as the M&M loop): half the taken branches per symbol
+                for (; k + 3 < mlo; k += 4) {   // uniform trip count
                     step(k, std::false_type{});
                     track();
                     step(k + 1, std::false_type{});
                     track();
+                    step(k + 2, std::false_type{});
+                    track();
+                    step(k + 3, std::false_type{});
+                    track();
+                }
+                if (k + 1 < mlo) {
+                    step(k, std::false_type{});
+                    track();
+                    step(k + 1, std::false_type{});
+                    track();
+                    k += 2;
                 }
                 if (k < mlo) {
                     step(k, std::false_type{});
