@@ -141,12 +141,16 @@ def _pipelined_rows(S, n, calls, sps, span, seed, idx, stats=None, **kw):
     b.set_stream(stream.cuda_stream)
     outs = []
     torch.cuda.synchronize(dev)
-    for k in range(calls):
-        x = iq[:, 2 * n * k: 2 * n * (k + 1)].contiguous()
-        bits = torch.zeros((S, (2 * ms + 7) // 8 + 8), dtype=torch.uint8, device=dev)
-        nb = torch.zeros(S, dtype=torch.int64, device=dev)
-        b.process_device_async(x, n, bits, nb)
-        outs.append((x, bits, nb))
+    # the input copies and the zeroed output rows on the handle's stream: made
+    # on torch's default stream they would race the handle's kernels (a
+    # test-harness race, seen once as a gate-test mismatch between two runs)
+    with torch.cuda.stream(stream):
+        for k in range(calls):
+            x = iq[:, 2 * n * k: 2 * n * (k + 1)].contiguous()
+            bits = torch.zeros((S, (2 * ms + 7) // 8 + 8), dtype=torch.uint8, device=dev)
+            nb = torch.zeros(S, dtype=torch.int64, device=dev)
+            b.process_device_async(x, n, bits, nb)
+            outs.append((x, bits, nb))
     b.pipeline_wait()
     torch.cuda.synchronize(dev)
     host = _rows(iq, idx)
