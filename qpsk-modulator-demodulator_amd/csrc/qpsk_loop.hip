@@ -111,6 +111,19 @@ __device__ __forceinline__ void swap_halves(double r, double *lower, double *upp
     *upper = __builtin_bit_cast(double, (static_cast<uint64_t>(ph[1]) << 32) | pl[1]);
 }
 
+// x or -x, i.e. x times +1.0 or -1.0 exactly: one v_cndmask_b32 with a
+// negated source on the high word.  The high word is made opaque as a float,
+// so the select keeps its fneg as a source modifier instead of becoming an
+// xor; in place when x dies at the select
+__device__ __forceinline__ double signsel(double x, bool pos) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, x);
+    float h = __builtin_bit_cast(float, static_cast<uint32_t>(b >> 32));
+    asm("" : "+v"(h));
+    const float r = pos ? h : -h;
+    return __builtin_bit_cast(double, (static_cast<uint64_t>(__builtin_bit_cast(uint32_t, r)) << 32) |
+                                          static_cast<uint32_t>(b));
+}
+
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
     const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), l);
     const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32), l);
@@ -146,11 +159,15 @@ struct LoopLds {
     static constexpr int RS = RowStride<CAP>::value;
     double tab[TRIG ? 880 : 1024];  // sincos table head, at LDS offset 0 so
     double tab_lo[TRIG ? 2 : 1024]; // the table index is the whole address; tail (floats, widened)
-    f2 mf[SPW * Ring<KB>::row];    // sample ring   [stream][mirror | 4 rounds x KB]
+    // the symbol slots sit below 64 KB, ahead of the ring: a ds instruction's
+    // immediate offset is 16 bits, so the Costas wave's per-step slot reads and
+    // writes then fold their constant part into the instruction instead of one
+    // v_add_u32 each (behind the 66 KB ring they did)
     sym_t sym[2 * SPW * RS];       // M&M -> Costas [slot][stream][RS] (see sym_t)
     typename std::conditional<ROTB, uint16_t, f2>::type rot[2 * SPW * RS];   // Costas -> decode
     int cnt[4 * SPW + 4];          // symbols produced by the M&M in round r: cnt[r & 3];
                                    // cnt[4*SPW + (r & 3)] = their minimum over the batch
+    alignas(16) f2 mf[SPW * Ring<KB>::row];   // sample ring [stream][mirror | 4 rounds x KB]
 };
 
 // SPW = streams (LDS rows) per workgroup; ACT >= SPW = lanes of the stage
@@ -463,6 +480,8 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const double did = ci >= 0.0f ? 1.0 : -1.0;
                 const double dqd = cq >= 0.0f ? 1.0 : -1.0;
                 const double cid = ci, cqd = cq;
+                // (dq * x as a sign select, signsel, measured one instruction
+                // longer here: the copy it needs of cqd's low word, twice)
                 const double t1 = fma(pdid, cid, pdqd * cqd);
                 const double t2 = fma(did, psid, dqd * psqd);
                 const double e = t1 - t2;
@@ -719,19 +738,34 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 const float ri = static_cast<float>(mi), rq = static_cast<float>(mq);
                 // e = +-1 (GetSign, :52-56): e*m is exact, so fma(ei, mq, -(eq*mi))
                 // rounds the same exact difference as the reference's subtraction
+                const bool qpos = rq >= 0.0f;
                 const double ei = ri >= 0.0f ? 1.0 : -1.0;
-                const double eq = rq >= 0.0f ? 1.0 : -1.0;
-                const double pe = fma(ei, mq, -(eq * mi));
+                // eq*mi is mi or -mi exactly: a select of mi's sign (one
+                // v_cndmask_b32 with a negated source, in place on the high
+                // word) instead of a +-1.0 double (a select plus a copy of its
+                // zero low word) and a multiply
+                const double qmi = signsel(mi, qpos);
+                const double pe = fma(ei, mq, -qmi);
                 freq = freq + cb * pe;
                 const double tn = theta + (freq + ca * pe);
                 // single +-2pi wrap (:89-91) as a select: tn - copysign(2pi, tn)
-                // is tn - 2pi above pi and tn + 2pi below -pi
-                const double tw = tn - copysign(kTwoPi, tn);
+                // is tn - 2pi above pi and tn + 2pi below -pi.  Computed as
+                // sign(tn) * (|tn| - 2pi), the same rounding (round-to-nearest-
+                // even is odd-symmetric): one add with an |abs| source and one
+                // xor of tn's sign into its high word, where copysign needed a
+                // bitfield insert plus a copy of 2pi's low word
+                const double u = fabs(tn) - kTwoPi;
+                const uint64_t ub = __builtin_bit_cast(uint64_t, u);
+                // v_bitop3 0x78 = src0 ^ (src1 & src2)
+                const uint32_t twh = __builtin_amdgcn_bitop3_b32(
+                    static_cast<uint32_t>(ub >> 32), static_cast<uint32_t>(__builtin_bit_cast(uint64_t, tn) >> 32), sgn_v, 0x78);
+                const double tw =
+                    __builtin_bit_cast(double, (static_cast<uint64_t>(twh) << 32) | static_cast<uint32_t>(ub));
                 theta = fabs(tn) > kPi ? tw : tn;
                 if constexpr (ROTB) {
                     // the decisions' sign bytes (byte 3 of the high words of +-1.0)
                     const uint32_t eih = static_cast<uint32_t>(__builtin_bit_cast(uint64_t, ei) >> 32);
-                    const uint32_t eqh = static_cast<uint32_t>(__builtin_bit_cast(uint64_t, eq) >> 32);
+                    const uint32_t eqh = qpos ? 0x3FF00000u : 0xBFF00000u;
                     out[k] = static_cast<uint16_t>(__builtin_amdgcn_perm(eqh, eih, 0x0c0c0703u));
                 } else {
                     out[k] = f2{ri, rq};
