@@ -352,6 +352,10 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         float psi = st.psi, psq = st.psq, pdi = st.pdi, pdq = st.pdq;
         int has_prev = mine ? st.has_prev : 1;
         const double sps = P.sps, kp = P.kp, ki = P.ki;
+        // the clamp bounds pinned in VGPRs: as SGPR pairs the compiler rebuilt
+        // -0.1 from 0.1's low word with an s_mov every symbol
+        double clamp_hi = 0.1, clamp_lo = -0.1;
+        asm volatile("" : "+v"(clamp_hi), "+v"(clamp_lo));
         const int cap = n;                          // output span = 2n floats (QPSKDeModulator.cs:366)
         int nsym = 0;
         bool stop = !mine;                          // capacity reached (MuellerMuller.cs:101-102)
@@ -491,7 +495,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 // the clamp as min/max: c > 0.1 -> 0.1, c < -0.1 -> -0.1 (a NaN c,
                 // which the reference cannot survive either, clamps instead of
                 // propagating)
-                const double corr = __builtin_fmax(__builtin_fmin(c, 0.1), -0.1);
+                const double corr = __builtin_fmax(__builtin_fmin(c, clamp_hi), clamp_lo);
                 out[k++] = to_sym(ci, cq, cid, cqd);
                 psid = cid; psqd = cqd;
                 pdid = did; pdqd = dqd;
