@@ -4,10 +4,11 @@
 // (CostasLoopQpsk.cs:63-92), the hard decision, differential decode and
 // MSB-first bit packing of QPSKDeModulator.DeModulate (QPSKDeModulator.cs:
 // 364-408).  Both loops are serial recurrences per stream, so a stream's work
-// cannot be spread over lanes; measured on MI355X (tools/loop_latency.hip) one
-// wave issues a dependent FP64 op every ~7.5 cycles and the per-symbol chains
-// are issue/latency-bound, so the lever is to give each stage of a stream its
-// OWN wave (its own SIMD issue port) and keep memory off the chains:
+// cannot be spread over lanes; measured on MI355X (tools/dep_probe.hip) one
+// wave issues one instruction per ~4 cycles, dependent or not, so a chain's
+// time per symbol is its instruction count x 4 plus its LDS round trips, and
+// the lever is to give each stage of a stream its OWN wave (its own SIMD issue
+// port) and keep memory off the chains:
 //
 //   workgroup = 4 waves, SPW streams (one lane each):
 //     wave 0  loader  HBM -> LDS ring of matched-filter samples with
