@@ -683,9 +683,6 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
         // otherwise each iteration rebuilds some from SGPR halves (VOP3 reads
         // one scalar operand), which costs issue slots on an issue-bound chain
         asm volatile("" : "+v"(ca), "+v"(cb), "+v"(kTwoPi), "+v"(kPi));
-        // the sign bit in a VGPR (v_bitop3_b32 takes no literal)
-        uint32_t sgn_v = 0x80000000u;
-        asm volatile("" : "+v"(sgn_v));
         asm volatile("" : "+v"(K.INV), "+v"(K.SH), "+v"(K.P1), "+v"(K.P2));
         asm volatile("" : "+v"(K.S3), "+v"(K.S5), "+v"(K.C4), "+v"(K.C6));
 #ifdef QPSK_LOOP_STAMPS
@@ -754,18 +751,12 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 freq = freq + cb * pe;
                 const double tn = theta + (freq + ca * pe);
                 // single +-2pi wrap (:89-91) as a select: tn - copysign(2pi, tn)
-                // is tn - 2pi above pi and tn + 2pi below -pi.  Computed as
-                // sign(tn) * (|tn| - 2pi), the same rounding (round-to-nearest-
-                // even is odd-symmetric): one add with an |abs| source and one
-                // xor of tn's sign into its high word, where copysign needed a
-                // bitfield insert plus a copy of 2pi's low word
-                const double u = fabs(tn) - kTwoPi;
-                const uint64_t ub = __builtin_bit_cast(uint64_t, u);
-                // v_bitop3 0x78 = src0 ^ (src1 & src2)
-                const uint32_t twh = __builtin_amdgcn_bitop3_b32(
-                    static_cast<uint32_t>(ub >> 32), static_cast<uint32_t>(__builtin_bit_cast(uint64_t, tn) >> 32), sgn_v, 0x78);
-                const double tw =
-                    __builtin_bit_cast(double, (static_cast<uint64_t>(twh) << 32) | static_cast<uint32_t>(ub));
+                // is tn - 2pi above pi and tn + 2pi below -pi.  (sign(tn) *
+                // (|tn| - 2pi) is one op shorter but gives -0 where the reference
+                // gives +0, at tn = -2pi; fma(copysign(1, tn), -2pi, tn) is exact
+                // too and measured 0.7 % slower at C2: tests/test_costas_identities.py,
+                // profiles/r05_costas_wrap_forms_ab.txt)
+                const double tw = tn - copysign(kTwoPi, tn);
                 theta = fabs(tn) > kPi ? tw : tn;
                 if constexpr (ROTB) {
                     // the decisions' sign bytes (byte 3 of the high words of +-1.0)
