@@ -149,6 +149,21 @@ __device__ __forceinline__ void band_prod(f2 T, f2 x, f2 &R, f2 &I) {
     R = add_xy_neghi(p, q);
     I = add_yx_neglo(p, q);
 }
+// The same products with the sign-split sums as one v_pk_fma_f32 each: q times
+// +-1 is exact, so fma(q, +-1, p) rounds p +- q once, as the reference's add or
+// subtraction (signed zeros, infinities and NaN alike); the compiler folds the
+// half-swizzles into op_sel.  Used for the partial sums, off the per-sample
+// chain: there they replace inline asm, which hipcc pads with an s_nop at each
+// boundary next to a dependent op and between consecutive statements (602 ->
+// 580 instructions per block with the scalar redo test, C5 FLL cycles per
+// sample -1.2 %, profiles/r05_fll_pkfma_ab.txt).  On the chain the asm form
+// measured faster.  KP = {1, -1}, KN = {-1, 1}, pinned in VGPRs by the caller.
+__device__ __forceinline__ void band_prod_fma(f2 T, f2 x, f2 KP, f2 KN, f2 &R, f2 &I) {
+    const f2 p = T.xx * x;   // {a xr, a xi}
+    const f2 q = T.yy * x;   // {b xr, b xi}
+    R = __builtin_elementwise_fma(q.yy, KP, p.xx);   // {p.x + q.y, p.x - q.y}
+    I = __builtin_elementwise_fma(q.xx, KN, p.yy);   // {p.y - q.x, p.y + q.x}
+}
 
 // one wave per SIMD (C5: 1024 waves on 1024 SIMDs): the whole VGPR file is
 // this wave's, so the scheduler need not keep 256 free for a second one
@@ -254,6 +269,10 @@ void fll_sys_kernel(FllArgs a, FllParams P) {
     partial(ring_at(0), 0);
 
     const float two_pi = 2.0f * 3.14159274101257324219f;
+    // the partial sums' sign vectors, pinned (as SGPR pairs the compiler
+    // rebuilt one from the other with two s_mov every block)
+    f2 KP = f2{1.0f, -1.0f}, KN = f2{-1.0f, 1.0f};
+    asm volatile("" : "+v"(KP), "+v"(KN));
     // the float sign bit in a VGPR for the sincos quadrant logic (v_bitop3_b32
     // takes no literal): pinned once here, not rebuilt every sample
     uint32_t sign_v = 0x80000000u;
@@ -387,7 +406,10 @@ void fll_sys_kernel(FllArgs a, FllParams P) {
     // x[t0 + u - 7]), so they are kept for a redo; step 8's (the next block's
     // step 0) reads x[t0] = G[p][0], the block's first output.
     f2 G[4][8];
-    bool need_exact = false;   // some lane's block-start phase is -0 (sincosf_split<false> excludes it)
+    // lanes whose block-start phase is -0 (sincosf_split<false> excludes it),
+    // as a ballot mask: the per-block redo test below is then two compares
+    // into SGPR masks, scalar ors and one branch on SCC
+    uint64_t need_exact = 0;
     auto rblock = [&](auto pc, const f2 *in, int64_t t0) __attribute__((always_inline)) {
         constexpr int p = decltype(pc)::value;
         auto X = [&](int k) __attribute__((always_inline)) -> f2 { return G[(p + (k >> 3)) & 3][k & 7]; };
@@ -398,11 +420,11 @@ void fll_sys_kernel(FllArgs a, FllParams P) {
         QI[0] = PI;
         auto part = [&](int u) __attribute__((always_inline)) {   // QR/QI[u + 1]
             f2 ar, ai;
-            band_prod(TT[0], X(u + 1), ar, ai);
+            band_prod_fma(TT[0], X(u + 1), KP, KN, ar, ai);
 #pragma unroll
             for (int j = 1; j < 4; ++j) {
                 f2 R, I;
-                band_prod(TT[j], X(u + 1 + 8 * j), R, I);
+                band_prod_fma(TT[j], X(u + 1 + 8 * j), KP, KN, R, I);
                 ar = ar + R;
                 ai = ai + I;
             }
@@ -438,7 +460,8 @@ void fll_sys_kernel(FllArgs a, FllParams P) {
             core(in[u], u, std::false_type{});
             part(u);
         }
-        if (__builtin_expect((__ballot((amax > two_pi) | (fmx > fmax_)) != 0) | need_exact, 0)) {
+        const uint64_t redo = __builtin_amdgcn_ballot_w64(amax > two_pi) | __builtin_amdgcn_ballot_w64(fmx > fmax_);
+        if (__builtin_expect((redo | need_exact) != 0, 0)) {
             // a wrap, a clamp or a -0 phase: redo the block exactly from its start
             phase = ph0; freq = fr0; SR = sr0; SI = si0;
 #pragma unroll
@@ -446,7 +469,7 @@ void fll_sys_kernel(FllArgs a, FllParams P) {
             part(7);
             // IEEERemainder can return -0 (an exact multiple of 2pi); a fast
             // block never creates -0 (x + y == -0 needs x == -0)
-            need_exact = __ballot(__float_as_uint(phase) == 0x80000000u) != 0;
+            need_exact = __builtin_amdgcn_ballot_w64(__float_as_uint(phase) == 0x80000000u);
         }
         PR = QR[8];
         PI = QI[8];
@@ -478,7 +501,7 @@ void fll_sys_kernel(FllArgs a, FllParams P) {
             G[k >> 2][(2 * k) & 7] = f2{v.x, v.y};
             G[k >> 2][(2 * k + 1) & 7] = f2{v.z, v.w};
         }
-        need_exact = __ballot(__float_as_uint(phase) == 0x80000000u) != 0;
+        need_exact = __builtin_amdgcn_ballot_w64(__float_as_uint(phase) == 0x80000000u);
         f2 A[8], B[8];
         load8(A, t0);
         load8(B, t0 + 8);
