@@ -533,59 +533,50 @@ QPSK_GHD static inline double qpsk_gl_with_hi(double v, uint32_t hi)
 
 QPSK_GHD static inline uint32_t qpsk_gl_hi(double v) { return (uint32_t)(qpsk_gl_bits(v) >> 32); }
 
-/* this half's argument of |x|; *t = n << 30 in region C (bit 31 = bit 1 of
- * n, bit 30 = bit 0), 0 elsewhere; *swap: the do_cos half's value is sin(|x|)
- * (region B, or region C with n odd) */
-QPSK_GHD static inline double qpsk_gl_fs_prepare(double x, const qpsk_gl_fs_lane *K, double *dxa, uint32_t *t,
-                                                 int *swap)
+/* the scheduler must not move the rest of the pair ahead of the row's loads */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define QPSK_GL_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define QPSK_GL_SCHED_BARRIER() ((void)0)
+#endif
+
+/* This half's value of the pair of x, with the sign it takes in the pair
+ * (do_sin on the K->sin_half lanes, do_cos on the others), and *swap: the
+ * do_cos half's value is sin(|x|) (region B, or region C with n odd).
+ *
+ * Region A runs as region C with n = 0: with the high word of 1/hp0 zeroed
+ * (a denormal), tt = toint exactly, xn = 0, and reduce_sincos returns
+ * (|x|, +0), which are region A's argument and dx bit for bit (-0 * c adds a
+ * signed zero to |x| or to +0), while tt's low word gives n = 0 (no swap, no
+ * quadrant sign).  The argument selects then have two ways instead of three.
+ *
+ * Order (round 5): the argument xa and the table row's address come first and
+ * the row's four loads are issued before anything else, behind a scheduling
+ * barrier, so the LDS round trip runs under dx, the quadrant logic and both
+ * polynomials instead of after them (tools/gl_costas_probe.hip). */
+QPSK_GHD static inline double qpsk_gl_fs_pair(double x, const qpsk_gl_fs_lane *K, const double *tabh, int *swap)
 {
     const double ax = fabs(x);
-    /* region C: reduce_sincos(|x|) */
-    const double tt = fma(ax, QPSK_GL_HPINV, K->toint);
+    const int rA = ax < 0x1.b6p-1;                   /* hi word < 0x3feb6000 */
+    const int rB = ax < 0x1.368fdp+1;                /* hi word < 0x400368fd */
+    const int rBo = rB && !rA;                       /* region B proper */
+    /* region C: reduce_sincos(|x|); region A: the same with n = 0 */
+    const uint64_t hpb = qpsk_gl_bits(QPSK_GL_HPINV);
+    const double hpinv = qpsk_gl_from_bits(rA ? (hpb & 0xffffffffull) : hpb);
+    const double tt = fma(ax, hpinv, K->toint);
     const double xn = tt - QPSK_GL_TOINT;
     double y = fma(-xn, QPSK_GL_MP1, ax);
     y = fma(-xn, QPSK_GL_MP2, y);
     const double t2 = fma(-xn, QPSK_GL_PP3, y);
-    double db = fma(-xn, QPSK_GL_PP3, y - t2);
     const double b = fma(-xn, QPSK_GL_PP4, t2);
-    db = db + fma(-xn, QPSK_GL_PP4, t2 - b);
     /* region B */
     const double yb = QPSK_GL_HP0 - ax;
     const double xb = yb + K->hp1L;
-    const double dB = (yb - xb) + QPSK_GL_HP1;
-    const int rA = ax < 0x1.b6p-1;                   /* hi word < 0x3feb6000 */
-    const int rB = ax < 0x1.368fdp+1;                /* hi word < 0x400368fd */
-    *dxa = rA ? 0.0 : (rB ? dB : db);
-    const uint32_t tn = (uint32_t)qpsk_gl_bits(tt) << 30;
-    *t = rB ? 0u : tn;
-    *swap = rA ? 0 : (rB ? 1 : (int)(tn >> 30) & 1);
-    return rA ? ax : (rB ? xb : b);
-}
-
-/* do_sin (K->sin_half) or do_cos of (xa, dxa), with the sign it takes in the
- * pair: t from qpsk_gl_fs_prepare */
-QPSK_GHD static inline double qpsk_gl_fs_half(double xa, double dxa, uint32_t t, const qpsk_gl_fs_lane *K,
-                                              const double *tabh)
-{
-    /* TAYLOR_SIN (qpsk_gl_taylor_sin) with the pinned addend */
-    const double ta = xa * xa;
-    double tp = fma(ta, QPSK_GL_S5, K->s4);
-    tp = fma(ta, tp, QPSK_GL_S3);
-    tp = fma(ta, tp, QPSK_GL_S2);
-    tp = fma(ta, tp, QPSK_GL_S1);
-    const double ty = xa + fma(ta, fma(tp, xa, -(0.5 * dxa)), dxa);
-    /* d = dx, negated when xa < 0 (xa is never -0): the sign of xa XORed in */
-    const double d = qpsk_gl_with_hi(dxa, qpsk_gl_hi(dxa) ^ (qpsk_gl_hi(xa) & K->sign));
-    const double ax = fabs(xa);
-    const double u = QPSK_GL_BIG + ax;
-    const double xr = fma(d, K->L1, ax - (u - QPSK_GL_BIG));
-    const double xx = xr * xr;
-    const double q = xr * xx;
-    const double p = fma(xx, QPSK_GL_SN5, K->sn3);
-    const double dl = d * K->L0;
-    const double s = fma(q, p, fma(xr, K->L1, dl)) + xr * K->L0;
-    const double c = fma(xr, dl, xx * fma(xx, fma(xx, QPSK_GL_CS6, K->cs4), QPSK_GL_CS2));
-    /* valid arguments give node <= 109; NaN any bits (stays in the table region) */
+    const double xa = rBo ? xb : b;
+    /* the table row: u = BIG + |xa| (valid arguments give node <= 109; NaN
+     * any bits, still inside the table) */
+    const double axa = fabs(xa);
+    const double u = QPSK_GL_BIG + axa;
     const uint32_t node = (uint32_t)qpsk_gl_bits(u) & 127u;
 #if defined(__HIP_DEVICE_COMPILE__)
     /* the table is in LDS: a 32-bit LDS address, node * 32 B + base in one op */
@@ -598,13 +589,39 @@ QPSK_GHD static inline double qpsk_gl_fs_half(double xa, double dxa, uint32_t t,
 #else
     const double *tb = tabh + 4 * node;
 #endif
-    double cor = fma(s, tb[0], tb[1]);
-    cor = fma(-c, tb[2], cor);
-    cor = fma(s, tb[3], cor);
-    const double r = tb[2] + cor;
+    const double T0 = tb[0], T1 = tb[1], T2 = tb[2], T3 = tb[3];
+    QPSK_GL_SCHED_BARRIER();
+    double db = fma(-xn, QPSK_GL_PP3, y - t2);
+    db = db + fma(-xn, QPSK_GL_PP4, t2 - b);
+    const double dB = (yb - xb) + QPSK_GL_HP1;
+    const double dxa = rBo ? dB : db;
+    /* n << 30: bit 31 = bit 1 of n, bit 30 = bit 0 (0 in region A) */
+    const uint32_t tn = (uint32_t)qpsk_gl_bits(tt) << 30;
+    const uint32_t t = rBo ? 0u : tn;
+    *swap = rBo ? 1 : (int)(tn >> 30) & 1;
+    /* TAYLOR_SIN (qpsk_gl_taylor_sin) with the pinned addend */
+    const double ta = xa * xa;
+    double tp = fma(ta, QPSK_GL_S5, K->s4);
+    tp = fma(ta, tp, QPSK_GL_S3);
+    tp = fma(ta, tp, QPSK_GL_S2);
+    tp = fma(ta, tp, QPSK_GL_S1);
+    const double ty = xa + fma(ta, fma(tp, xa, -(0.5 * dxa)), dxa);
+    /* d = dx, negated when xa < 0 (xa is never -0): the sign of xa XORed in */
+    const double d = qpsk_gl_with_hi(dxa, qpsk_gl_hi(dxa) ^ (qpsk_gl_hi(xa) & K->sign));
+    const double xr = fma(d, K->L1, axa - (u - QPSK_GL_BIG));
+    const double xx = xr * xr;
+    const double q = xr * xx;
+    const double p = fma(xx, QPSK_GL_SN5, K->sn3);
+    const double dl = d * K->L0;
+    const double s = fma(q, p, fma(xr, K->L1, dl)) + xr * K->L0;
+    const double c = fma(xr, dl, xx * fma(xx, fma(xx, QPSK_GL_CS6, K->cs4), QPSK_GL_CS2));
+    double cor = fma(s, T0, T1);
+    cor = fma(-c, T2, cor);
+    cor = fma(s, T3, cor);
+    const double r = T2 + cor;
     /* do_sin: copysign(r, xa) (r > 0); do_sin below 0.126: TAYLOR_SIN */
     double v = qpsk_gl_with_hi(r, qpsk_gl_bfi(K->sgnm, qpsk_gl_hi(xa), qpsk_gl_hi(r)));
-    if (K->sin_half && ax < 0.126) v = ty;
+    if (K->sin_half && axa < 0.126) v = ty;
     /* the pair's sign of this value (region C) */
     return qpsk_gl_with_hi(v, qpsk_gl_hi(v) ^ ((t + K->tsh) & K->sign));
 }
@@ -623,13 +640,9 @@ QPSK_GHD static inline void qpsk_glibc_sincos_fs_host(double x, const double *ta
                                                       double *s_out, double *c_out)
 {
     const qpsk_gl_fs_lane k0 = qpsk_gl_fs_lane_init(1), k1 = qpsk_gl_fs_lane_init(0);
-    double d0, d1;
-    uint32_t t0, t1;
     int w0, w1;
-    const double x0 = qpsk_gl_fs_prepare(x, &k0, &d0, &t0, &w0);
-    const double x1 = qpsk_gl_fs_prepare(x, &k1, &d1, &t1, &w1);
-    const double VS = qpsk_gl_fs_half(x0, d0, t0, &k0, tabs);
-    const double VC = qpsk_gl_fs_half(x1, d1, t1, &k1, tabc);
+    const double VS = qpsk_gl_fs_pair(x, &k0, tabs, &w0);
+    const double VC = qpsk_gl_fs_pair(x, &k1, tabc, &w1);
     qpsk_gl_fs_finish(x, w0, VS, VC, &k0, s_out, c_out);
 }
 

@@ -718,11 +718,8 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 // Math.Sin/Cos = glibc; the fast pass leaves its Payne-Hanek reduction out
                 if constexpr (TRIG && !decltype(huge)::value) {
                     // the fast pass: the pair of |theta| (qpsk_glibc_trig.h, fast split form)
-                    double dxa;
-                    uint32_t tq;
                     int sw;
-                    const double xa = qpsk_gl_fs_prepare(theta, &KF, &dxa, &tq, &sw);
-                    const double rh = qpsk_gl_fs_half(xa, dxa, tq, &KF, tabh);
+                    const double rh = qpsk_gl_fs_pair(theta, &KF, tabh, &sw);
                     double VS, VC;
                     swap_halves(rh, &VS, &VC);
                     qpsk_gl_fs_finish(theta, sw, VS, VC, &KF, &sn, &cs);
