@@ -712,8 +712,13 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             // C3 batch has 27 such streams after 6 calls; with the old 1e6 range
             // their 26 workgroups redid every round and the kernel took 2.7x)
             auto widen = [](sym_t v) { return from_sym(v); };
+            // the previous step's decisions, stored under this step's table loads
+            // (row entry CAP, past the round's symbols, takes the first store)
+            typename std::remove_reference<decltype(out[0])>::type pend{};
+            int pend_k = CAP;
+            double amax = fabs(theta);   // largest sincos argument of the round
+            auto track = [&]() { asm volatile("v_max_f64 %0, %0, |%1|" : "+v"(amax) : "v"(theta)); };
             auto step = [&](int k, auto huge) {
-                const d2 yn = widen(in[k + 1]);   // next symbol, read and widened under this one's chain
                 double sn, cs;
                 // Math.Sin/Cos = glibc; the fast pass leaves its Payne-Hanek reduction out
                 if constexpr (TRIG && !decltype(huge)::value) {
@@ -731,7 +736,23 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                     qpsk_gl_split_finish(theta, &g, DS, DC, &sn, &cs);
                 }
                 else if constexpr (decltype(huge)::value) qpsk_sincos_tab(theta, L.tab, L.tab_lo, &sn, &cs);
-                else qpsk_sincos_tab_core_k(theta, L.tab, L.tab_lo, &K, &sn, &cs);
+                else {
+                    // the table row's loads first; under their LDS round trip the
+                    // previous step's store, |theta| of its result (this step's
+                    // argument) and the next symbol's read, then the polynomials
+                    const qpsk_sincos_row row = qpsk_sincos_tab_load(theta, L.tab, L.tab_lo, &K);
+                    __builtin_amdgcn_sched_barrier(0);
+                    out[pend_k] = pend;
+                    track();
+                    __builtin_amdgcn_sched_barrier(0);
+                    qpsk_sincos_tab_eval(&row, &K, &sn, &cs);
+                }
+                if constexpr (TRIG || decltype(huge)::value) {
+                    // after the trig (the glibc pair issues its row's loads first)
+                    out[pend_k] = pend;
+                    track();
+                }
+                const d2 yn = widen(in[k + 1]);   // next symbol, read under this one's chain
                 const double mi = y.x * cs + y.y * sn;
                 const double mq = y.y * cs - y.x * sn;
                 const float ri = static_cast<float>(mi), rq = static_cast<float>(mq);
@@ -759,43 +780,34 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                     // the decisions' sign bytes (byte 3 of the high words of +-1.0)
                     const uint32_t eih = static_cast<uint32_t>(__builtin_bit_cast(uint64_t, ei) >> 32);
                     const uint32_t eqh = qpos ? 0x3FF00000u : 0xBFF00000u;
-                    out[k] = static_cast<uint16_t>(__builtin_amdgcn_perm(eqh, eih, 0x0c0c0703u));
+                    pend = static_cast<uint16_t>(__builtin_amdgcn_perm(eqh, eih, 0x0c0c0703u));
                 } else {
-                    out[k] = f2{ri, rq};
+                    pend = f2{ri, rq};
                 }
+                pend_k = k;
                 y = yn;
             };
             const double theta0 = theta, freq0 = freq;
             y = widen(in[0]);
             int k = 0;
-            double amax = fabs(theta);   // largest sincos argument of the round
             STAMP(tu);
             if (m >= mlo) {              // every stream the M&M ran uniformly
-                // one v_max_f64 (fmax would first canonicalize amax)
-                auto track = [&]() { asm volatile("v_max_f64 %0, %0, |%1|" : "+v"(amax) : "v"(theta)); };
                 // an even unroll: y and the next symbol alternate registers
                 // instead of being copied back every symbol
                 // by four (as the M&M loop): half the taken branches per symbol
                 for (; k + 3 < mlo; k += 4) {   // uniform trip count
                     step(k, std::false_type{});
-                    track();
                     step(k + 1, std::false_type{});
-                    track();
                     step(k + 2, std::false_type{});
-                    track();
                     step(k + 3, std::false_type{});
-                    track();
                 }
                 if (k + 1 < mlo) {
                     step(k, std::false_type{});
-                    track();
                     step(k + 1, std::false_type{});
-                    track();
                     k += 2;
                 }
                 if (k < mlo) {
                     step(k, std::false_type{});
-                    track();
                     ++k;
                 }
             }
@@ -803,10 +815,9 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
 #ifdef QPSK_LOOP_STAMPS
             k_uit += mlo;
 #endif
-            for (; k < m; ++k) {         // per-lane remainder (~1 symbol)
-                step(k, std::false_type{});
-                amax = fmax(amax, fabs(theta));
-            }
+            for (; k < m; ++k) step(k, std::false_type{});   // per-lane remainder (~1 symbol)
+            out[pend_k] = pend;          // the round's last step
+            track();
             // fmax drops NaN, which the fast path handles exactly like the full one
             // the fast pass's range: |theta| <= 2^40 (portable table), < 105414348
             // (glibc without __branred)
@@ -816,6 +827,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 freq = freq0;
                 y = widen(in[0]);
                 for (k = 0; k < m; ++k) step(k, std::true_type{});
+                out[pend_k] = pend;
             }
             ACC(k_loop, tl);
         }

@@ -28,6 +28,11 @@
 #else
 #define QPSK_HD
 #endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#define QPSK_SINCOS_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define QPSK_SINCOS_SCHED_BARRIER() ((void)0)
+#endif
 
 /* [2k] = sin(k pi/256), [2k+1] = cos(k pi/256), k < 512: correctly rounded
  * double + float tail (tools/gen_sincos_table.py) */
@@ -67,8 +72,14 @@ typedef struct {
         0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10   /* 1/24, -1/720 */          \
     }
 
-QPSK_HD static inline void qpsk_sincos_tab_core_k(double x, const double *tab, const double *lo,
-                                             const qpsk_sincos_consts *K, double *s, double *c)
+/* the table row of x and the shifted multiple (first half of the core) */
+typedef struct {
+    double x, kb;
+    double ts, tc, ls, lc;
+} qpsk_sincos_row;
+
+QPSK_HD static inline qpsk_sincos_row qpsk_sincos_tab_load(double x, const double *tab, const double *lo,
+                                                           const qpsk_sincos_consts *K)
 {
     /* kb = fma(x, 256/pi, 1.5*2^52) rounds the exact product to an integer
      * (ties to even), so k = kb - 1.5*2^52 = rint(x*256/pi) exactly
@@ -76,12 +87,24 @@ QPSK_HD static inline void qpsk_sincos_tab_core_k(double x, const double *tab, c
      * complement: the table index without a separate rint */
     union { double d; unsigned long long u; } kb;
     kb.d = fma(x, K->INV, K->SH);
-    const double k = kb.d - K->SH;
-    double r = fma(-k, K->P1, x);                  /* Cody-Waite: |r| <= pi/512 */
-    r = fma(-k, K->P2, r);
     const unsigned i = (unsigned)(kb.u & 511u) * 2u;
-    const double ts = tab[i], tc = tab[i + 1];
-    const double ls = lo[i], lc = lo[i + 1];
+    qpsk_sincos_row R;
+    R.x = x;
+    R.kb = kb.d;
+    R.ts = tab[i];
+    R.tc = tab[i + 1];
+    R.ls = lo[i];
+    R.lc = lo[i + 1];
+    return R;
+}
+
+/* the second half: reduction, polynomials, angle addition */
+QPSK_HD static inline void qpsk_sincos_tab_eval(const qpsk_sincos_row *R, const qpsk_sincos_consts *K, double *s,
+                                                double *c)
+{
+    const double k = R->kb - K->SH;
+    double r = fma(-k, K->P1, R->x);               /* Cody-Waite: |r| <= pi/512 */
+    r = fma(-k, K->P2, r);
     /* sin r = r + r^3(-1/6 + r^2/120), cos r - 1 = r^2(-1/2 + r^2/24 - r^4/720):
      * truncation < 1e-19 relative for |r| <= pi/512 */
     const double z = r * r;
@@ -89,8 +112,19 @@ QPSK_HD static inline void qpsk_sincos_tab_core_k(double x, const double *tab, c
     const double cm = z * fma(z, fma(z, K->C6, K->C4), -0.5);   /* cos r - 1 */
     /* angle addition, small terms first: sin x = ts + [tc r + (tc r3p + ts cm + ls)],
      * one significant rounding in the bracket and one in the final add: <= 1 ulp */
-    *s = ts + fma(tc, r, fma(tc, r3p, fma(ts, cm, ls)));
-    *c = tc + fma(-ts, r, fma(-ts, r3p, fma(tc, cm, lc)));
+    *s = R->ts + fma(R->tc, r, fma(R->tc, r3p, fma(R->ts, cm, R->ls)));
+    *c = R->tc + fma(-R->ts, r, fma(-R->ts, r3p, fma(R->tc, cm, R->lc)));
+}
+
+/* both halves; on the GPU the row's loads go out first: the scheduler may not
+ * move the reduction or the polynomials ahead of them (a GPU caller with work
+ * of its own for the LDS round trip calls the halves itself) */
+QPSK_HD static inline void qpsk_sincos_tab_core_k(double x, const double *tab, const double *lo,
+                                             const qpsk_sincos_consts *K, double *s, double *c)
+{
+    const qpsk_sincos_row R = qpsk_sincos_tab_load(x, tab, lo, K);
+    QPSK_SINCOS_SCHED_BARRIER();
+    qpsk_sincos_tab_eval(&R, K, s, c);
 }
 
 /* sin and cos of x, |x| <= 2^40 or NaN, given the 512-entry table (any address
