@@ -460,6 +460,10 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 if constexpr (decltype(load)::value) {
                     tp = taps_fl(fl);
                     xm1 = tp[0]; x0 = tp[1]; x1 = tp[2]; x2 = tp[3];
+                    // the tap loads go out before anything after them in the
+                    // source (the step's symbol store, the next interpolation's
+                    // coefficients), which then runs under their LDS round trip
+                    __builtin_amdgcn_sched_barrier(0);
                 }
             };
             auto reload = [&]() {
@@ -497,10 +501,11 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 // which the reference cannot survive either, clamps instead of
                 // propagating)
                 const double corr = __builtin_fmax(__builtin_fmin(c, clamp_hi), clamp_lo);
-                out[k++] = to_sym(ci, cq, cid, cqd);
                 psid = cid; psqd = cqd;
                 pdid = did; pdqd = dqd;
                 advance(sps + corr, load);
+                // stored after the next taps' loads (LDS serves in issue order)
+                out[k++] = to_sym(ci, cq, cid, cqd);
 #ifdef QPSK_LOOP_STAMPS
                 ++c_iters;
 #endif
