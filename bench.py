@@ -285,7 +285,8 @@ def portable_check(iq, bits_dev, nbits_dev, syms_dev, nsyms_dev, cfg, idx, costa
         gns = rows_to_host(nsyms_dev, idx)
         for i in range(len(idx)):
             ns = int(rns[i])
-            if int(gns[i]) != ns or not np.array_equal(gsy[i, : 2 * ns], rsy[i, : 2 * ns]):
+            if int(gns[i]) != ns or not np.array_equal(gsy[i, : 2 * ns].view(np.uint32),
+                                                      rsy[i, : 2 * ns].view(np.uint32)):
                 sym_bad += 1
     return len(bad), sym_bad
 
@@ -518,6 +519,118 @@ def host_ring_pass(demod, iq, S, n, steps=6, warmup=2, depth=2):
             "ms_per_call": round(dt / steps * 1e3, 3), "depth": depth, "steps": steps,
             "h2d_GBps": round(8.0 * S * n * steps / dt / 1e9, 2),
             "note": "host pinned slots -> H2D -> demod -> D2H bits, calls overlapped; not the headline value"}
+
+
+def s1_host_leg(dev, steps=10, warmup=2):
+    """The literal drop-in shape (INTEGRATION.md's QPSKDeModulator shim): ONE
+    stream per handle, 2^20 samples at sps 8 / 65 taps from host memory through
+    qpsk_demod_process(MEM_HOST), one synchronous call after another, as
+    ModDemodOverSDR.cs:136 calls DeModulate.  Timed with the host clock around
+    the calls (PCIe upload, FIR, symbol loop, bits back), beside the CPU
+    oracle's single core on the same row; the first call's bits are checked
+    against the oracle."""
+    import numpy as np
+    import qpsk_amd as Q
+    import oracle as O
+    cfg = CONFIGS["c2"]
+    n = 1 << 20
+    rs = FS // cfg["sps"]
+    iq, _ = Q.synth_generate(1, n, FS, rs, rrc_alpha=ALPHA, rrc_span=cfg["span"], seed=0x5159534B,
+                             lo_ppm=1.0, device=dev.index)
+    row = iq.cpu().numpy()
+    del iq
+    d = Q.BatchDemodulator(1, Q.params(FS, rs, ALPHA, cfg["span"], device=dev.index, max_samples_per_call=n))
+    bits, nb, _, _ = d.process(row)
+    first = (bits.copy(), nb.copy())
+    for _ in range(warmup - 1):
+        d.process(row)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        d.process(row)
+    dt = time.perf_counter() - t0
+    d.close()
+    t1 = time.perf_counter()
+    rb, rnb, _, _ = O.demod_batch_packed(row, FS, rs, n_threads=1, rrc_alpha=ALPHA, rrc_span=cfg["span"],
+                                         trig=O.TRIG_LIBM)
+    dt1 = time.perf_counter() - t1
+    bad, _ = compare_rows(first[0], first[1], rb, rnb)
+    return {"kind": "drop_in", "value": round(n * steps / dt / 1e6, 2), "unit": "MSa/s",
+            "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps, "warmup": warmup,
+            "config": {"workload": "1 stream x 2^20 samples, sps 8, 65 taps, host memory, "
+                                   "qpsk_demod_process(MEM_HOST) with S = 1 (the INTEGRATION.md shim)"},
+            "cpu_single_core": round(n / dt1 / 1e6, 2),
+            "parity": {"libm_oracle": {"streams": 1, "mismatching": len(bad)}},
+            "note": "one stream per handle: the symbol loop is one serial recurrence on one lane, so the "
+                    "GPU runs it at its per-symbol latency; batch streams per handle (BatchDeModulator, "
+                    "INTEGRATION.md) for the batched rates"}
+
+
+def host_ring_c3_leg(dev, chunk=1 << 18, steps=2, warmup=1):
+    """C3 fed from host memory through the pinned ring (qpsk_rx_*, the
+    ModDemodOverSDR.cs:116-183 receive loop at batch scale): 4096 streams x
+    2^20 samples per step, uploaded in chunks of `chunk` samples per stream
+    (4 chunks a step), each chunk's upload overlapping the previous chunk's
+    demod.  The ring has one pinned slot per chunk, filled once before the
+    timed region straight from the GPU-synthesised batch (an SDR driver would
+    DMA into them), so every step replays the same 2^20 samples per stream.
+    PCIe-inclusive: not the headline value.  The first chunk's bits of the
+    first and last stream are checked against the oracle."""
+    import numpy as np
+    import torch
+    import qpsk_amd as Q
+    import oracle as O
+    cfg = CONFIGS["c3"]
+    S, n = cfg["streams"], 1 << 20
+    rs = FS // cfg["sps"]
+    k = n // chunk
+    iq, _ = Q.synth_generate(S, n, FS, rs, rrc_alpha=ALPHA, rrc_span=cfg["span"], seed=0x5159534B,
+                             lo_ppm=1.0, device=dev.index)
+    d = Q.BatchDemodulator(S, Q.params(FS, rs, ALPHA, cfg["span"], device=dev.index, max_samples_per_call=chunk))
+    ring = Q.HostRing(d, k)
+    host0 = iq[[0, S - 1], : 2 * chunk].cpu().numpy()
+    for j in range(k):                     # slot j <- chunk j of every stream (D2H into pinned memory)
+        slot = torch.from_numpy(ring.next_slot())
+        slot[:, : 2 * chunk].copy_(iq[:, 2 * chunk * j: 2 * chunk * (j + 1)])
+        ring.submit(None, chunk)
+    torch.cuda.synchronize(dev)
+    del iq
+    torch.cuda.empty_cache()
+    bits0, nb0, _ = ring.collect()        # chunk 0 from the fresh state
+    check = (bits0[[0, S - 1]].copy(), nb0[[0, S - 1]].copy())
+    pending = k - 1
+    for _ in range(warmup * k):
+        if pending == k:
+            ring.collect()
+            pending -= 1
+        ring.submit(None, chunk)
+        pending += 1
+    while pending:
+        ring.collect()
+        pending -= 1
+    t0 = time.perf_counter()
+    for _ in range(steps * k):
+        if pending == k:
+            ring.collect()
+            pending -= 1
+        ring.submit(None, chunk)
+        pending += 1
+    while pending:
+        ring.collect()
+        pending -= 1
+    dt = time.perf_counter() - t0
+    ring.close()
+    d.close()
+    rb, rnb, _, _ = O.demod_batch_packed(host0, FS, rs, n_threads=2, rrc_alpha=ALPHA, rrc_span=cfg["span"],
+                                         trig=O.TRIG_LIBM)
+    bad, _ = compare_rows(check[0], check[1], rb, rnb)
+    return {"kind": "drop_in", "value": round(S * n * steps / dt / 1e6, 2), "unit": "MSa/s",
+            "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps, "warmup": warmup,
+            "config": {"workload": f"C3 from host memory: {S} streams x 2^20 samples per step through the "
+                                   f"pinned ring (qpsk_rx_*), {k} chunks of {chunk} samples per stream, "
+                                   f"depth {k}"},
+            "h2d_GBps": round(8.0 * S * n * steps / dt / 1e9, 2),
+            "parity": {"libm_oracle": {"streams": 2, "mismatching": len(bad)}},
+            "note": "PCIe-inclusive (8 B/sample up, bits down); not the headline value"}
 
 
 def framer_pass(bits, nbits, S, stream, reps=5):
@@ -853,7 +966,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
                    "streams_per_gpu": S, "samples_per_stream": n,
                    "sps": sps, "taps": span * sps + 1, "fll": cfg["fll"],
                    "parallelism": f"stream-shard x{world}",
-                   "costas_trig": "glibc sin/cos (bit-exact)" if trig else
+                   "costas_trig": "glibc sin/cos (bit-exact vs glibc libm)" if trig else
                                   "portable table sincos (<= 1 ulp from glibc)",
                    "calls": "serial" if args.serial_calls else
                             f"pipelined (front/back stage overlap, depth {demod.pipeline_depth()})"},
@@ -1001,7 +1114,11 @@ def compact_record(out, detail_name):
     for key, r in (out.get("sub_records") or {}).items():
         s = {k: r[k] for k in ("value", "ms_per_step", "steps", "warmup") if k in r}
         s["workload"] = r.get("config", {}).get("workload")
-        s.update(_compact_body(r))
+        if r.get("kind") == "drop_in":
+            # the drop-in's own shapes (host memory): their few fields as they are
+            s.update({k: r[k] for k in ("unit", "cpu_single_core", "h2d_GBps", "parity", "error") if k in r})
+        else:
+            s.update(_compact_body(r))
         subs[key] = s
     if subs:
         line["sub_records"] = subs
@@ -1019,6 +1136,18 @@ def dump_line(line):
             break
         line = dict(line, sub_records={key: {k: v for k, v in r.items() if keep(k)}
                                        for key, r in line["sub_records"].items()})
+        s = json.dumps(line, separators=(",", ":"))
+    # still too long (an oversized headline, or no sub-records to trim): the
+    # driver would drop the whole line unparsed, so fall back to the driver's
+    # keys, roofline, cpu_baseline and the detail-file name, and say so
+    for keys in (HEAD_KEYS + ("roofline", "cpu_baseline", "parity", "detail"),
+                 HEAD_KEYS + ("roofline", "cpu_baseline", "detail"), HEAD_KEYS + ("detail",)):
+        if len(s) <= LINE_MAX_BYTES:
+            break
+        sys.stderr.write(f"bench.py: stdout line {len(s)} B > {LINE_MAX_BYTES} B; keeping only "
+                         f"{', '.join(keys)} (the detail file has everything)\n")
+        line = {k: line[k] for k in keys if k in line}
+        line["truncated"] = True
         s = json.dumps(line, separators=(",", ":"))
     return s
 
@@ -1065,6 +1194,9 @@ def main():
                          "traces, so its kernel averages are the timed region's")
     ap.add_argument("--no-host-ring", action="store_true",
                     help="skip the PCIe-inclusive host-ring pass (N=1, batches <= 4 GiB: C2)")
+    ap.add_argument("--no-drop-in", action="store_true",
+                    help="skip the drop-in shape legs (N=1: one stream per handle from host memory, C3 "
+                         "through the pinned host ring)")
     ap.add_argument("--no-framer", action="store_true",
                     help="skip the device TSC + framer pass measured beside the headline")
     ap.add_argument("--no-split-gather", action="store_true",
@@ -1079,7 +1211,7 @@ def main():
     args = ap.parse_args()
     if args.timed_only:
         args.no_parity = args.no_framer = args.no_split_gather = True
-        args.no_host_ring = args.no_cpu_baseline = True
+        args.no_host_ring = args.no_cpu_baseline = args.no_drop_in = True
         args.sub_configs = "none"
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -1117,6 +1249,15 @@ def main():
         for k in ("metric", "unit", "n_gpus", "higher_is_better", "scaling", "vs_baseline", "dtype"):
             r.pop(k, None)
         sub[key] = r
+    if world == 1 and not args.no_drop_in:
+        # the drop-in's own shapes, host memory in: one stream
+        # per handle, and C3 through the pinned ring.  PCIe-inclusive, never `value`
+        for key, leg in (("s1_host", s1_host_leg), ("host_ring_c3", host_ring_c3_leg)):
+            try:
+                sub[key] = leg(dev)
+            except Exception as e:       # a failed side leg must not cost the headline line
+                sub[key] = {"kind": "drop_in", "error": f"{type(e).__name__}: {e}"[:300]}
+            torch.cuda.empty_cache()
     if sub:
         out["sub_records"] = sub
     if world > 1 and not args.no_split_gather:

@@ -27,11 +27,13 @@
 extern "C" {
 #endif
 
-/* 2: versioned state blob (header + length checked by set_state; 256-sample
+/* 3: multi-GPU group (qpsk_shard_streams, qpsk_demod_group_*); no change to
+ *    existing entry points or the state blob.
+ * 2: versioned state blob (header + length checked by set_state; 256-sample
  *    M&M carry), get_state / set_state take the buffer length and a non-const
  *    handle (they flush pipelined work), qpsk_pipeline_gate_enabled.
  * 1: rounds 1-3. */
-#define QPSK_ABI_VERSION 2
+#define QPSK_ABI_VERSION 3
 
 /* status codes -> the C# exception each one replaces */
 #define QPSK_OK 0
@@ -189,7 +191,15 @@ int qpsk_demod_process_async(qpsk_demod *h, int32_t mode, const float *iq, int64
  * it off (the list above); needs no device. */
 int qpsk_pipeline_gate_enabled(void);
 /* Residency-gate waits of this handle that ran out (QPSK_GATE_TIMEOUT_MS) since
- * it was created, after every queued call; 0 in normal operation. */
+ * it was created, after every queued call; 0 in normal operation.  Besides
+ * serialised dispatch, contention can also run a wait out: at most one loop
+ * workgroup fits a CU (its LDS), so another handle's or process's loop kernel
+ * holding every CU for longer than the cap delays this one's workgroups past
+ * it.  Nothing hangs and no result changes; only the overlap order of that
+ * call may differ.  Raise QPSK_GATE_TIMEOUT_MS where handles share a GPU with
+ * long calls.  (QPSK_GATE_NO_PUBLISH=1 is a test hook that suppresses the
+ * count so every wait runs out; it is honoured only together with
+ * QPSK_PIPELINE_GATE=1.) */
 int qpsk_demod_gate_timeouts(qpsk_demod *h, uint64_t *count);
 /* The symbol-loop shape qpsk_demod_create picks for loop_variant = 0 (auto):
  * at sps >= 8, 7 (6 streams x 512-sample rounds) while ceil(S/6) <= cus, else
@@ -281,6 +291,54 @@ int qpsk_demod_design(const qpsk_demod_params *p, float *rrc_taps, int32_t cap, 
 int64_t qpsk_demod_state_bytes(const qpsk_demod *h);
 int qpsk_demod_get_state(qpsk_demod *h, void *host_buf, int64_t buf_bytes);
 int qpsk_demod_set_state(qpsk_demod *h, const void *host_buf, int64_t buf_bytes);
+
+/* ---------------------------------------------------------------------------
+ * Multi-GPU group: one batch of n_streams over several GPUs,
+ * for a host (the C# shim, a C++ driver) that wants the whole node behind one
+ * object.  Every reference instance owns its loop state (QPSKDeModulator.cs:20-73),
+ * so the batch splits into contiguous shards with no exchange: shard k =
+ * streams [n*k/n_dev, n*(k+1)/n_dev) on devices[k], one ordinary handle each
+ * (the split bench.py's ranks use).  A group call slices the caller's rows by
+ * row offset (shard k reads iq + first_k*stride_floats, lengths + first_k and
+ * writes bits + first_k*bits_stride_bytes, n_bits + first_k, syms + ..., n_syms
+ * + ...), runs every shard at once on its own worker thread, and returns when
+ * all are done.  Results equal one handle's over the whole batch, stream for
+ * stream.  One caller thread per group, as for a handle.
+ */
+typedef struct qpsk_demod_group qpsk_demod_group;
+/* Contiguous shard k of n_parts over n_streams: *first = n_streams*k/n_parts,
+ * *count = n_streams*(k+1)/n_parts - *first.  Needs no device. */
+int qpsk_shard_streams(int32_t n_streams, int32_t n_parts, int32_t k, int32_t *first, int32_t *count);
+/* n_dev handles with params p (p->device ignored: shard k lives on devices[k];
+ * a device may repeat, e.g. two shards on device 0).  n_streams >= n_dev. */
+int qpsk_demod_group_create(const qpsk_demod_params *p, const int32_t *devices, int32_t n_dev,
+                            int32_t n_streams, qpsk_demod_group **out);
+/* Waits for every shard's work, destroys the handles, stops the workers. */
+int qpsk_demod_group_destroy(qpsk_demod_group *g);
+/* Number of shards (n_dev). */
+int qpsk_demod_group_size(const qpsk_demod_group *g);
+/* Shard k's first stream, stream count, device and handle (any may be NULL).
+ * The handle belongs to the group; use it for device-resident batches on a
+ * multi-GPU group (pointers on that shard's device), streams, timing. */
+int qpsk_demod_group_shard(const qpsk_demod_group *g, int32_t k, int32_t *first_stream, int32_t *n_streams,
+                           int32_t *device, qpsk_demod **handle);
+/* qpsk_demod_process on every shard, fanned out and joined; arguments as for
+ * one handle over all n_streams rows.  mem = QPSK_MEM_HOST (the C# spans) on
+ * any group; QPSK_MEM_DEVICE only when every shard is on one device (else
+ * QPSK_ERR_ARGUMENT: call the shard handles), and the call then returns with
+ * the outputs written (each shard's stream is joined).  Arguments are checked
+ * on the whole batch before any shard runs; a shard that fails later returns
+ * its status with "shard k (device d): ..." in qpsk_last_error, the other
+ * shards' calls having run (as independent C# instances would). */
+int qpsk_demod_group_process(qpsk_demod_group *g, int32_t mode, const float *iq, int64_t stride_floats,
+                             int64_t n_samples, const int64_t *lengths, int32_t mem, uint8_t *bits,
+                             int64_t bits_stride_bytes, int64_t *n_bits, float *syms, int64_t syms_stride_floats,
+                             int64_t *n_syms);
+/* Per-shard checkpoint / migration: qpsk_demod_state_bytes / get_state /
+ * set_state of shard k's handle (0 bytes for a bad k). */
+int64_t qpsk_demod_group_state_bytes(const qpsk_demod_group *g, int32_t k);
+int qpsk_demod_group_get_state(qpsk_demod_group *g, int32_t k, void *host_buf, int64_t buf_bytes);
+int qpsk_demod_group_set_state(qpsk_demod_group *g, int32_t k, const void *host_buf, int64_t buf_bytes);
 
 /* ---------------------------------------------------------------------------
  * Host-fed streaming front-end: the deployment shape of

@@ -509,7 +509,13 @@ void fll_sys_kernel(FllArgs a, FllParams P) {
         // and the compiler's vmcnt model of the loop body is the steady state's
         // (from the preheader it would assume A's loads were followed by B's
         // only, and wait for nearly every load of the first blocks)
-        __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0), expcnt / lgkmcnt not waited
+        // 0xF70 = vmcnt(0) with expcnt / lgkmcnt not waited under the gfx9
+        // s_waitcnt field layout only; another target's layout would wait on
+        // the wrong counters without a word from the compiler
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "qpsk_fll.hip: the raw s_waitcnt immediate assumes gfx950 (gfx9 field layout)"
+#endif
+        __builtin_amdgcn_s_waitcnt(0xF70);
         do {
             rblock(std::integral_constant<int, 0>{}, A, t0);
             load8(A, t0 + 16);

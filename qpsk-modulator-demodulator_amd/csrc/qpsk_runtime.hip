@@ -191,8 +191,9 @@ struct qpsk_demod {
     bool use_gate = true;
     // the wait is bounded (gate_wait_kernel): at most gate_cap_ticks of the
     // wall clock (QPSK_GATE_TIMEOUT_MS, default 2000 ms), counted in d_gate[0]
-    // when it runs out; gate_publish = false (QPSK_GATE_NO_PUBLISH=1, tests
-    // only) keeps the loop workgroups from counting, so every wait runs out
+    // when it runs out; gate_publish = false (QPSK_GATE_NO_PUBLISH=1 together
+    // with QPSK_PIPELINE_GATE=1, tests only) keeps the loop workgroups from
+    // counting, so every wait runs out
     unsigned *d_gate = nullptr;
     unsigned long long gate_cap_ticks = 0;
     bool gate_publish = true;
@@ -215,6 +216,7 @@ hipStream_t pipe_front_stream(const qpsk_demod *h) { return h->s_front; }
 int handle_streams(const qpsk_demod *h) { return h->S; }
 int64_t handle_max_samples(const qpsk_demod *h) { return h->n_max; }
 int handle_device(const qpsk_demod *h) { return h->p.device; }
+int handle_sync(qpsk_demod *h);   // below: every queued call of the handle done
 }  // namespace qpsk
 
 namespace {
@@ -267,6 +269,9 @@ int validate(qpsk_demod *h, Call &c) {
         return fail(QPSK_ERR_ARGUMENT, "device stride_floats must be even");
     int rc;
     if (c.syms && !h->d_syms) {
+        // on the handle's device whatever the calling thread's current one is
+        // (a group's worker threads, qpsk_group.cpp)
+        HIP_TRY(hipSetDevice(h->p.device));
         if ((rc = dev_alloc(&h->d_syms, static_cast<size_t>(2 * S * h->syms_cap)))) return rc;
     }
     c.n_call = n_call;
@@ -484,37 +489,46 @@ namespace {
 // latency-bound stage, the front stage fills the CUs it leaves idle.
 int pipe_setup(qpsk_demod *h) {
     if (h->pipe_ready) return QPSK_OK;
+    // every step is guarded: a set-up that failed part way runs again on the
+    // next pipelined call and completes what is missing, leaking nothing and
+    // keeping (not re-zeroing) the counters it already made
     int least = 0, greatest = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    HIP_TRY(hipStreamCreateWithPriority(&h->s_front, hipStreamNonBlocking, least));
-    HIP_TRY(hipStreamCreateWithPriority(&h->s_back, hipStreamNonBlocking, greatest));
-    HIP_TRY(hipEventCreateWithFlags(&h->e_in, hipEventDisableTiming));
+    if (!h->s_front) HIP_TRY(hipStreamCreateWithPriority(&h->s_front, hipStreamNonBlocking, least));
+    if (!h->s_back) HIP_TRY(hipStreamCreateWithPriority(&h->s_back, hipStreamNonBlocking, greatest));
+    if (!h->e_in) HIP_TRY(hipEventCreateWithFlags(&h->e_in, hipEventDisableTiming));
     for (int b = 0; b < 2; ++b) {
-        HIP_TRY(hipEventCreateWithFlags(&h->e_front[b], hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&h->e_back[b], hipEventDisableTiming));
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h->h_len[b]), h->S * sizeof(int64_t)));
+        if (!h->e_front[b]) HIP_TRY(hipEventCreateWithFlags(&h->e_front[b], hipEventDisableTiming));
+        if (!h->e_back[b]) HIP_TRY(hipEventCreateWithFlags(&h->e_back[b], hipEventDisableTiming));
+        if (!h->h_len[b]) HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h->h_len[b]), h->S * sizeof(int64_t)));
     }
-    HIP_TRY(hipEventCreateWithFlags(&h->e_fll, hipEventDisableTiming));
-    HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void **>(&h->d_resident), sizeof(unsigned long long),
-                                  hipMallocSignalMemory));
-    HIP_TRY(hipMemset(h->d_resident, 0, sizeof(unsigned long long)));
+    if (!h->e_fll) HIP_TRY(hipEventCreateWithFlags(&h->e_fll, hipEventDisableTiming));
+    if (!h->d_resident) {
+        HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void **>(&h->d_resident), sizeof(unsigned long long),
+                                      hipMallocSignalMemory));
+        HIP_TRY(hipMemset(h->d_resident, 0, sizeof(unsigned long long)));
+    }
     int rc;
-    if ((rc = dev_alloc(&h->d_gate, 1))) return rc;
-    HIP_TRY(hipMemset(h->d_gate, 0, sizeof(unsigned)));
+    if (!h->d_gate) {
+        if ((rc = dev_alloc(&h->d_gate, 1))) return rc;
+        HIP_TRY(hipMemset(h->d_gate, 0, sizeof(unsigned)));
+    }
     if (!h->d_lengths[1] && (rc = dev_alloc(&h->d_lengths[1], h->S))) return rc;
     // the second boundary buffer: MF rows (the FIR of one call writes one while
     // the loop kernel of the previous call reads the other).  No room for it
     // (batches near the 288 GB) -> calls still queue back to back, but each
     // front stage waits for the previous back stage
     const size_t S = static_cast<size_t>(h->S);
-    hipError_t e = hipMalloc(reinterpret_cast<void **>(&h->d_mf[1]), 2 * S * h->mf_stride * sizeof(float));
-    if (e == hipSuccess) {
-        h->pipe_bufs = 2;
-        HIP_TRY(hipMemset(h->d_mf[1], 0, 2 * S * h->mf_stride * sizeof(float)));
-    } else {
-        (void)hipGetLastError();
-        h->pipe_bufs = 1;
+    if (!h->d_mf[1]) {
+        hipError_t e = hipMalloc(reinterpret_cast<void **>(&h->d_mf[1]), 2 * S * h->mf_stride * sizeof(float));
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            h->d_mf[1] = nullptr;
+        } else {
+            HIP_TRY(hipMemset(h->d_mf[1], 0, 2 * S * h->mf_stride * sizeof(float)));
+        }
     }
+    h->pipe_bufs = h->d_mf[1] ? 2 : 1;
     h->pipe_ready = true;
     return QPSK_OK;
 }
@@ -653,8 +667,12 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
         const char *v = std::getenv("QPSK_GATE_TIMEOUT_MS");
         const long ms = v && *v ? std::strtol(v, nullptr, 10) : 2000;
         h->gate_cap_ticks = static_cast<unsigned long long>(ms > 0 ? ms : 1) * static_cast<unsigned>(h->wall_khz);
+        // test hook, honoured only beside an explicit QPSK_PIPELINE_GATE=1: a
+        // stray QPSK_GATE_NO_PUBLISH alone must not make every call wait out the cap
         const char *np = std::getenv("QPSK_GATE_NO_PUBLISH");
-        h->gate_publish = !(np && *np && std::strcmp(np, "0") != 0);
+        const char *force = std::getenv("QPSK_PIPELINE_GATE");
+        const bool forced = force && std::strcmp(force, "1") == 0;
+        h->gate_publish = !(forced && np && *np && std::strcmp(np, "0") != 0);
     }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup_fail(fail(QPSK_ERR_DEVICE, "hipStreamCreate failed"));
@@ -705,6 +723,7 @@ int qpsk_demod_create(const qpsk_demod_params *p, int32_t n_streams, qpsk_demod 
 
 int qpsk_demod_destroy(qpsk_demod *h) {
     if (!h) return QPSK_OK;
+    (void)hipSetDevice(h->p.device);   // frees and stream teardown on the handle's device
     drain_async(h);
     if (h->stream) hipStreamSynchronize(h->stream);
     hipFree(h->d_hrev);
@@ -747,6 +766,7 @@ int qpsk_demod_destroy(qpsk_demod *h) {
 
 int qpsk_demod_set_stream(qpsk_demod *h, void *hip_stream) {
     if (!h) return fail(QPSK_ERR_ARGUMENT_NULL, "null handle");
+    HIP_TRY(hipSetDevice(h->p.device));
     int rc;
     if ((rc = drain_async(h))) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1199,6 +1219,18 @@ int process_chunked(qpsk_demod *h, const Call &c, bool async) {
 
 }  // namespace (calls)
 
+namespace qpsk {
+// The host waits for every call queued on the handle, pipelined or stream-ordered
+// (the multi-device group's join, qpsk_group.cpp).
+int handle_sync(qpsk_demod *h) {
+    int rc;
+    if ((rc = drain_async(h))) return rc;
+    HIP_TRY(hipSetDevice(h->p.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return QPSK_OK;
+}
+}  // namespace qpsk
+
 extern "C" {
 
 int qpsk_demod_process(qpsk_demod *h, int32_t mode, const float *iq, int64_t stride_floats,
@@ -1244,6 +1276,7 @@ int qpsk_demod_status(qpsk_demod *h, uint32_t *flags) {
     if (!h || !flags) return fail(QPSK_ERR_ARGUMENT_NULL, "null argument");
     int rc;
     if ((rc = drain_async(h))) return rc;
+    HIP_TRY(hipSetDevice(h->p.device));
     HIP_TRY(hipStreamSynchronize(h->stream));
     HIP_TRY(hipMemcpy(h->h_flags, h->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemset(h->d_flags, 0, sizeof(uint32_t)));
@@ -1363,6 +1396,7 @@ int qpsk_demod_get_state(qpsk_demod *h, void *host_buf, int64_t buf_bytes) {
     char *p = static_cast<char *>(host_buf);
     int rc;
     if ((rc = drain_async(h))) return rc;
+    HIP_TRY(hipSetDevice(h->p.device));
     HIP_TRY(hipStreamSynchronize(h->stream));
     const StateHeader hd = state_header(h);
     std::memcpy(p, &hd, sizeof(hd));
@@ -1398,6 +1432,7 @@ int qpsk_demod_set_state(qpsk_demod *h, const void *host_buf, int64_t buf_bytes)
     const char *p = static_cast<const char *>(host_buf) + sizeof(StateHeader);
     int rc;
     if ((rc = drain_async(h))) return rc;
+    HIP_TRY(hipSetDevice(h->p.device));
     HIP_TRY(hipStreamSynchronize(h->stream));
     HIP_TRY(hipMemcpy(h->d_state, p, S * sizeof(StreamState), hipMemcpyHostToDevice));
     p += S * sizeof(StreamState);

@@ -211,6 +211,21 @@ def lib():
     L.qpsk_rx_submit.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, _i64p,
                                  C.POINTER(C.c_int64)]
     L.qpsk_rx_collect.argtypes = [C.c_void_p, _u8p, C.c_int64, _i64p, C.POINTER(C.c_int64)]
+    L.qpsk_shard_streams.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32),
+                                     C.POINTER(C.c_int32)]
+    L.qpsk_demod_group_create.argtypes = [C.POINTER(DemodParams), C.POINTER(C.c_int32), C.c_int32, C.c_int32,
+                                          C.POINTER(C.c_void_p)]
+    L.qpsk_demod_group_destroy.argtypes = [C.c_void_p]
+    L.qpsk_demod_group_size.argtypes = [C.c_void_p]
+    L.qpsk_demod_group_shard.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_int32), C.POINTER(C.c_void_p)]
+    L.qpsk_demod_group_process.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64, C.c_int64,
+                                           _i64p, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p,
+                                           C.c_void_p, C.c_int64, C.c_void_p]
+    L.qpsk_demod_group_state_bytes.argtypes = [C.c_void_p, C.c_int32]
+    L.qpsk_demod_group_state_bytes.restype = C.c_int64
+    L.qpsk_demod_group_get_state.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64]
+    L.qpsk_demod_group_set_state.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64]
     _lib = real
     return real
 
@@ -234,6 +249,9 @@ EXPORTED_SYMBOLS = [
     "qpsk_rx_next_slot", "qpsk_rx_submit", "qpsk_rx_collect", "qpsk_demod_status", "qpsk_demod_last_mf",
     "qpsk_mod_params_init", "qpsk_mod_create", "qpsk_mod_destroy", "qpsk_mod_set_stream",
     "qpsk_mod_output_floats", "qpsk_mod_modulate", "qpsk_mod_modulate_bytes",
+    "qpsk_shard_streams", "qpsk_demod_group_create", "qpsk_demod_group_destroy", "qpsk_demod_group_size",
+    "qpsk_demod_group_shard", "qpsk_demod_group_process", "qpsk_demod_group_state_bytes",
+    "qpsk_demod_group_get_state", "qpsk_demod_group_set_state",
 ]
 
 _EXC = {
@@ -511,6 +529,103 @@ class BatchDemodulator:
         v = C.c_uint64()
         _check(lib().qpsk_demod_gate_timeouts(self._h, C.byref(v)))
         return v.value
+
+
+def shard_streams(n_streams: int, n_parts: int, k: int):
+    """(first, count) of contiguous shard k of n_parts (qpsk_shard_streams;
+    needs no device)."""
+    f, c = C.c_int32(), C.c_int32()
+    _check(lib().qpsk_shard_streams(int(n_streams), int(n_parts), int(k), C.byref(f), C.byref(c)))
+    return f.value, c.value
+
+
+class DemodGroup:
+    """One batch of streams over several GPUs (qpsk_demod_group_*): shard k =
+    contiguous streams on devices[k], one handle each, fanned out per call on
+    worker threads and joined.  process() takes the same host rows as
+    BatchDemodulator.process over all n_streams and returns the same arrays."""
+
+    def __init__(self, n_streams: int, p: DemodParams, devices):
+        self.S = int(n_streams)
+        self.p = p
+        devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+        g = C.c_void_p()
+        _check(lib().qpsk_demod_group_create(C.byref(p), devs, len(devices), self.S, C.byref(g)))
+        self._g = g
+        # for max_symbols (every shard has the same params)
+        self._h0 = self.shard(0)[3]
+
+    def close(self):
+        if getattr(self, "_g", None):
+            lib().qpsk_demod_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self) -> int:
+        return _check(lib().qpsk_demod_group_size(self._g))
+
+    def shard(self, k: int):
+        """(first_stream, n_streams, device, raw handle) of shard k."""
+        f, n, d, h = C.c_int32(), C.c_int32(), C.c_int32(), C.c_void_p()
+        _check(lib().qpsk_demod_group_shard(self._g, int(k), C.byref(f), C.byref(n), C.byref(d), C.byref(h)))
+        return f.value, n.value, d.value, h
+
+    def max_symbols(self, n: int) -> int:
+        return int(lib().qpsk_demod_max_symbols(self._h0, int(n)))
+
+    def get_state(self, k: int) -> bytes:
+        n = lib().qpsk_demod_group_state_bytes(self._g, int(k))
+        buf = C.create_string_buffer(n)
+        _check(lib().qpsk_demod_group_get_state(self._g, int(k), buf, n))
+        return buf.raw
+
+    def set_state(self, k: int, blob: bytes):
+        buf = C.create_string_buffer(bytes(blob), len(blob))
+        _check(lib().qpsk_demod_group_set_state(self._g, int(k), buf, len(blob)))
+
+    def process(self, iq: np.ndarray, mode=MODE_DEMODULATE, lengths=None, want_syms=False):
+        """iq: [S, 2n] float32 host rows of the whole batch; returns (bits,
+        n_bits, syms or None, n_syms) exactly as BatchDemodulator.process."""
+        iq = np.ascontiguousarray(iq, dtype=np.float32)
+        if iq.ndim != 2 or iq.shape[0] != self.S or iq.shape[1] & 1:
+            raise ValueError("iq must be [n_streams, 2*n]")
+        n = iq.shape[1] // 2
+        if lengths is not None:
+            lengths = np.ascontiguousarray(lengths, dtype=np.int64)
+            nmax = int(lengths.max()) if lengths.size else 0
+        else:
+            nmax = n
+        ms = max(self.max_symbols(nmax), 1)
+        bstride = (2 * ms + 7) // 8 + 8
+        bits = np.zeros((self.S, bstride), dtype=np.uint8)
+        n_bits = np.zeros(self.S, dtype=np.int64)
+        n_syms = np.zeros(self.S, dtype=np.int64)
+        syms = np.zeros((self.S, 2 * ms), dtype=np.float32) if (want_syms or mode == MODE_CONSTELLATION) else None
+        _check(lib().qpsk_demod_group_process(
+            self._g, int(mode), iq.ctypes.data if iq.size else None, iq.shape[1], n,
+            lengths.ctypes.data_as(_i64p) if lengths is not None else None, MEM_HOST,
+            bits.ctypes.data if mode == MODE_DEMODULATE else None, bstride,
+            n_bits.ctypes.data if mode == MODE_DEMODULATE else None,
+            syms.ctypes.data if syms is not None else None, 2 * ms, n_syms.ctypes.data))
+        return bits, n_bits, syms, n_syms
+
+    def process_device(self, iq_dev, n, bits_dev, n_bits_dev, mode=MODE_DEMODULATE, syms_dev=None,
+                       n_syms_dev=None):
+        """Device rows of the whole batch (every shard on one device): returns
+        with the outputs written."""
+        bstride = bits_dev.stride(0) * bits_dev.element_size() if bits_dev is not None else 0
+        sstride = syms_dev.stride(0) if syms_dev is not None else 0
+        _check(lib().qpsk_demod_group_process(
+            self._g, int(mode), iq_dev.data_ptr(), iq_dev.stride(0), int(n), None, MEM_DEVICE,
+            bits_dev.data_ptr() if bits_dev is not None else None, bstride,
+            n_bits_dev.data_ptr() if n_bits_dev is not None else None,
+            syms_dev.data_ptr() if syms_dev is not None else None, sstride,
+            n_syms_dev.data_ptr() if n_syms_dev is not None else None))
 
 
 class HostRing:

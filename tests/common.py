@@ -54,3 +54,24 @@ def batch_signals(n_streams, seed0=0, **kw):
 
 def oracle_for(sps, span, **kw):
     return O.OracleDemod(FS, FS // sps, ALPHA, span, **kw)
+
+
+def bitwise_equal(a, b, nan_any_payload=False):
+    """Exact float parity: same dtype, shape and bit patterns, so -0 vs +0 and
+    NaN payloads count (np.array_equal treats +-0 as equal and never matches a
+    NaN).  nan_any_payload: NaN must meet NaN at the same positions, but its
+    payload may differ (the default NaN of an invalid operation is 0xFFC00000 on
+    x86, where the oracle runs, and 0x7FC00000 on gfx950); every other value
+    still compares bit for bit."""
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    if a.dtype != b.dtype or a.shape != b.shape:
+        return False
+    if a.dtype.kind != "f":
+        return bool(np.array_equal(a, b))
+    u = {2: np.uint16, 4: np.uint32, 8: np.uint64}[a.dtype.itemsize]
+    if nan_any_payload:
+        na, nb = np.isnan(a), np.isnan(b)
+        if not np.array_equal(na, nb):
+            return False
+        return bool(np.array_equal(a[~na].view(u), b[~nb].view(u)))
+    return bool(np.array_equal(a.view(u), b.view(u)))

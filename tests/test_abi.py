@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.check_output(["nm", "-D", "--defined-only", Q.LIB_PATH]).decode()
     for n in names:
         assert re.search(r"\bT " + n + r"\b", out), n
-    assert L.qpsk_abi_version() == 2
+    assert L.qpsk_abi_version() == 3
 
 
 def test_library_has_gfx950_code_object():

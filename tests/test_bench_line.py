@@ -64,6 +64,43 @@ def test_canned_full_run_line_is_bounded_and_complete():
         assert f'"{k}"' not in s, k
 
 
+DROP_IN = {
+    "s1_host": {"kind": "drop_in", "value": 61.2, "unit": "MSa/s", "ms_per_step": 17.1, "steps": 10, "warmup": 2,
+                "config": {"workload": "1 stream x 2^20 samples, sps 8, 65 taps, host memory, "
+                                       "qpsk_demod_process(MEM_HOST) with S = 1 (the INTEGRATION.md shim)"},
+                "cpu_single_core": 59.5, "parity": {"libm_oracle": {"streams": 1, "mismatching": 0}},
+                "note": "x" * 300},
+    "host_ring_c3": {"kind": "drop_in", "value": 6500.0, "unit": "MSa/s", "ms_per_step": 660.0, "steps": 2,
+                     "warmup": 1, "h2d_GBps": 52.0,
+                     "config": {"workload": "C3 from host memory: 4096 streams x 2^20 samples per step through "
+                                            "the pinned ring (qpsk_rx_*), 4 chunks of 262144 samples per "
+                                            "stream, depth 4"},
+                     "parity": {"libm_oracle": {"streams": 2, "mismatching": 0}}, "note": "y" * 300},
+}
+
+
+def test_full_line_with_drop_in_records_stays_bounded_untrimmed():
+    """The round-6 line: the four config sub-records plus the two drop-in
+    shapes (s1_host, host_ring_c3) fit the 12 KB bound with nothing trimmed:
+    every sub-record keeps its kernel table, and the drop-in records keep
+    value, cpu_single_core and parity."""
+    full = canned()
+    full["sub_records"].update(copy.deepcopy(DROP_IN))
+    line = bench.compact_record(full, "bench_detail.json")
+    untrimmed = json.dumps(line, separators=(",", ":"))
+    s = bench.dump_line(line)
+    assert s == untrimmed and len(s) <= bench.LINE_MAX_BYTES, len(untrimmed)
+    got = json.loads(s)["sub_records"]
+    assert got["s1_host"]["cpu_single_core"] == 59.5 and got["s1_host"]["value"] == 61.2
+    assert got["s1_host"]["parity"]["libm_oracle"]["mismatching"] == 0
+    assert got["host_ring_c3"]["h2d_GBps"] == 52.0
+    assert "note" not in got["s1_host"] and "kernels" in got["c2"]
+    # a leg that failed keeps its error text in the line
+    full["sub_records"]["s1_host"] = {"kind": "drop_in", "error": "RuntimeError: boom"}
+    got = json.loads(bench.dump_line(bench.compact_record(full, "d.json")))["sub_records"]
+    assert got["s1_host"]["error"] == "RuntimeError: boom"
+
+
 def test_oversized_sub_records_are_trimmed_not_fatal():
     full = canned()
     for i in range(40):
@@ -73,6 +110,25 @@ def test_oversized_sub_records_are_trimmed_not_fatal():
     assert len(s) <= bench.LINE_MAX_BYTES
     assert line["value"] == full["value"] and "roofline" in line and "cpu_baseline" in line
     assert all("value" in r for r in line["sub_records"].values())
+
+
+def test_oversized_headline_falls_back_to_driver_keys(capsys):
+    """A headline too big by itself (nothing left to trim in sub-records) is
+    cut down to the driver's keys + roofline + cpu_baseline, with a warning on
+    stderr, instead of leaving the driver an unparsable line."""
+    full = canned()
+    full.pop("sub_records")
+    full["config"] = dict(full["config"], padding="x" * 20_000)   # the driver's own keys overflow
+    s = bench.dump_line(bench.compact_record(full, "d.json"))
+    line = json.loads(s)
+    assert line["truncated"] is True and line["detail"] == "d.json"
+    assert line["value"] == full["value"] and "metric" in line
+    assert "bench.py: stdout line" in capsys.readouterr().err
+    full["config"] = dict(full["config"], padding="x")
+    full["stages_ms"] = {f"k{i}": i for i in range(2000)}            # a bloated body only
+    line = json.loads(bench.dump_line(bench.compact_record(full, "d.json")))
+    assert len(json.dumps(line, separators=(",", ":"))) <= bench.LINE_MAX_BYTES
+    assert "roofline" in line and "cpu_baseline" in line and line["truncated"] is True
 
 
 def test_missing_legs_serialise():

@@ -79,15 +79,15 @@ def test_oracle_and_refmodel_reproduce_tad_sps8():
     sps, span = int(z["sps"]), int(z["span"])
     iq = z["iq"]
     b, s, _ = K.oracle_for(sps, span).demodulate_ex(iq)
-    assert b == bits_str(z["bits"]) and np.array_equal(s, z["syms"])
+    assert b == bits_str(z["bits"]) and K.bitwise_equal(s, z["syms"])
     bl, sl, _ = K.oracle_for(sps, span, trig=O.TRIG_LIBM).demodulate_ex(iq)
-    assert bl == b and np.array_equal(sl, z["syms_libm"])
+    assert bl == b and K.bitwise_equal(sl, z["syms_libm"])
     assert np.max(np.abs(sl - s)) <= 1e-5
     m = RM.RefDemod(K.FS, K.FS // sps, K.ALPHA, span)
     rb, rot, mf = m.demodulate(iq)
     assert rb == b
     assert np.array_equal(rot, s)
-    assert np.array_equal(mf[: z["mf_head"].size], z["mf_head"])
+    assert K.bitwise_equal(mf[: z["mf_head"].size], z["mf_head"])
 
 
 def test_oracle_reproduces_impaired():
@@ -102,7 +102,7 @@ def test_oracle_reproduces_impaired():
             dm = K.oracle_for(sps, span, enable_fll=fll)
             for a, e in ((0, cut[s]), (cut[s], n)):
                 b, y, _ = dm.demodulate_ex(iq[s, 2 * a: 2 * e])
-                assert b == bits_str(bits[i]) and np.array_equal(y, syms[i])
+                assert b == bits_str(bits[i]) and K.bitwise_equal(y, syms[i])
                 i += 1
 
 
@@ -140,7 +140,7 @@ def test_gpu_tad_literal_raw_symbols(Q):
     for f, r, s in zip(frames, split(z["raw_bits"], z["raw_bits_len"]), split(z["syms"], z["syms_len"])):
         bits, nb, syms, ns = b.process(f[None, :], want_syms=True)
         assert Q.unpack_bits(bits[0], int(nb[0])) == bits_str(r)
-        assert np.array_equal(syms[0, : 2 * int(ns[0])], s)
+        assert K.bitwise_equal(syms[0, : 2 * int(ns[0])], s)
     b.close()
 
 
@@ -151,7 +151,7 @@ def test_gpu_tad_sps8(Q):
     b = Q.BatchDemodulator(1, Q.params(K.FS, K.FS // sps, K.ALPHA, span, max_samples_per_call=iq.size // 2))
     bits, nb, syms, ns = b.process(iq[None, :], want_syms=True)
     assert Q.unpack_bits(bits[0], int(nb[0])) == bits_str(z["bits"])
-    assert np.array_equal(syms[0, : 2 * int(ns[0])], z["syms"])
+    assert K.bitwise_equal(syms[0, : 2 * int(ns[0])], z["syms"])
     assert np.max(np.abs(syms[0, : 2 * int(ns[0])] - z["syms_libm"])) <= 1e-5
     b.close()
     # the Costas NCO on glibc's own sin/cos: the libm fixture, bit for bit
@@ -159,7 +159,7 @@ def test_gpu_tad_sps8(Q):
                                        costas_trig=1))
     bits, nb, syms, ns = b.process(iq[None, :], want_syms=True)
     assert Q.unpack_bits(bits[0], int(nb[0])) == bits_str(z["bits"])
-    assert np.array_equal(syms[0, : 2 * int(ns[0])], z["syms_libm"])
+    assert K.bitwise_equal(syms[0, : 2 * int(ns[0])], z["syms_libm"])
     b.close()
 
 
@@ -184,5 +184,5 @@ def test_gpu_impaired_ragged(Q, tag, fll):
         for s in range(S):
             i = 2 * s + call
             assert Q.unpack_bits(gb[s], int(nb[s])) == bits_str(bits[i]), f"stream {s} call {call}"
-            assert np.array_equal(gs[s, : 2 * int(ns[s])], syms[i]), f"stream {s} call {call}"
+            assert K.bitwise_equal(gs[s, : 2 * int(ns[s])], syms[i]), f"stream {s} call {call}"
     b.close()

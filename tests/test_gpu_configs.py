@@ -122,7 +122,7 @@ def test_baseline_workload_seven_calls_vs_libm_oracle(key, trig):
                 g = gsy[: 2 * int(gns)]
                 assert g.shape == rsy.shape, f"{key} stream {s} call {k}: symbol count"
                 if exact:
-                    assert np.array_equal(g, rsy), f"{key} stream {s} call {k}: symbols"
+                    assert K.bitwise_equal(g, rsy), f"{key} stream {s} call {k}: symbols (bitwise)"
                 else:
                     assert np.max(np.abs(g - rsy), initial=0) <= SYM_TOL, f"{key} stream {s} call {k}"
 

@@ -82,7 +82,7 @@ def assert_same(a, b, exact=True):
                 continue
             assert sa.shape == sb.shape, f"call {ci} stream {s}: symbol count"
             if exact:
-                assert np.array_equal(sa, sb), f"call {ci} stream {s}: symbols differ"
+                assert K.bitwise_equal(sa, sb), f"call {ci} stream {s}: symbols differ (bitwise)"
             else:
                 assert np.max(np.abs(sa - sb), initial=0) <= SYM_TOL
 
@@ -446,7 +446,7 @@ def test_huge_amplitude_takes_the_costas_rollback_path():
     for ci, (ra, rb) in enumerate(zip(got, ref)):
         for s, ((ba, sa), (bb, sb)) in enumerate(zip(ra, rb)):
             assert ba == bb, f"call {ci} stream {s}: bits differ"
-            assert np.array_equal(sa.view(np.uint32), sb.view(np.uint32)), f"call {ci} stream {s}"
+            assert K.bitwise_equal(sa, sb), f"call {ci} stream {s}"
     # (with |pe| ~ 1e12 the first symbol already moves freq by cb*pe ~ 1e10, so
     # theta leaves [-1e6, 1e6] within a round)
 
@@ -472,7 +472,7 @@ def test_degenerate_streams_bit_exact(sps, span):
     for ci, (ra, rb) in enumerate(zip(got, ref)):
         for s, ((ba, sa), (bb, sb)) in enumerate(zip(ra, rb)):
             assert ba == bb, f"call {ci} stream {s}: bits differ"
-            assert np.array_equal(sa.view(np.uint32), sb.view(np.uint32)), f"call {ci} stream {s}: symbols"
+            assert K.bitwise_equal(sa, sb), f"call {ci} stream {s}: symbols"
 
 
 def ring_run(iq2d, calls, sps, span, depth=2, zero_copy=False, **kw):

@@ -50,7 +50,7 @@ def test_rows_past_4gib_bit_exact():
     for i, s in enumerate(idx):
         ob, osy, _ = K.oracle_for(8, 8).demodulate_ex(host[i])
         assert Q.unpack_bits(gb[i], int(gnb[i])) == ob, f"stream {s}: bits"
-        assert np.array_equal(gs[i, : 2 * int(gns[i])], osy), f"stream {s}: symbols"
+        assert K.bitwise_equal(gs[i, : 2 * int(gns[i])], osy), f"stream {s}: symbols"
     assert b.status() == 0
     b.close()
 
@@ -96,7 +96,7 @@ def test_call_longer_than_capacity_is_chunked(ragged):
         m = int(lens[s]) if ragged else n
         ob, osy, _ = K.oracle_for(8, 8).demodulate_ex(iq[s, : 2 * m])
         assert Q.unpack_bits(bits[s], int(nb[s])) == ob, f"stream {s}: bits"
-        assert np.array_equal(syms[s, : 2 * int(ns[s])], osy), f"stream {s}: symbols"
+        assert K.bitwise_equal(syms[s, : 2 * int(ns[s])], osy), f"stream {s}: symbols"
     b.close()
 
 
@@ -129,7 +129,7 @@ def test_chunked_device_and_pipelined_calls():
             for s in range(S):
                 rb, rs = ref[ci][s]
                 assert Q.unpack_bits(bits[s].cpu().numpy(), int(nb[s])) == rb, (pipelined, ci, s)
-                assert np.array_equal(sy[s, : 2 * int(ns[s])].cpu().numpy(), rs), (pipelined, ci, s)
+                assert K.bitwise_equal(sy[s, : 2 * int(ns[s])].cpu().numpy(), rs), (pipelined, ci, s)
         b.close()
 
 
@@ -156,7 +156,7 @@ def test_nonfinite_samples_in_the_matched_filter():
     taps_iq[0::2] = taps
     for s in range(S):
         ref = O.oracle_fir(taps_iq, iq[s])
-        assert np.array_equal(mf[s], ref, equal_nan=True), f"stream {s}"
+        assert K.bitwise_equal(mf[s], ref, nan_any_payload=True), f"stream {s}"
         if s > 0:
             assert np.isnan(mf[s]).any()
     assert b.status() & Q.STATUS_NONFINITE_TIMING
