@@ -565,6 +565,49 @@ def s1_host_leg(dev, steps=10, warmup=2):
                     "INTEGRATION.md) for the batched rates"}
 
 
+def batch_host_leg(dev, steps=5, warmup=1):
+    """INTEGRATION.md's BatchDeModulator on host spans: C2's 256 streams x 2^20
+    samples from ordinary (pageable) host memory per synchronous call, through
+    one handle (qpsk_demod_process(MEM_HOST)) and through a group of two shards
+    on the same GPU (qpsk_demod_group_process), whose shards' uploads and
+    computes overlap each other.  Host clock around the calls; the two paths'
+    bit rows of the last call are compared with each other, row for row."""
+    import numpy as np
+    import qpsk_amd as Q
+    cfg = CONFIGS["c2"]
+    S, n = cfg["streams"], 1 << 20
+    rs = FS // cfg["sps"]
+    iq, _ = Q.synth_generate(S, n, FS, rs, rrc_alpha=ALPHA, rrc_span=cfg["span"], seed=0x5159534B,
+                             lo_ppm=1.0, device=dev.index)
+    host = iq.cpu().numpy()
+    del iq
+    p = Q.params(FS, rs, ALPHA, cfg["span"], device=dev.index, max_samples_per_call=n)
+    rates, rows = {}, {}
+    for name, make in (("one_handle", lambda: Q.BatchDemodulator(S, p)),
+                       ("group_2x_same_gpu", lambda: Q.DemodGroup(S, p, [dev.index, dev.index]))):
+        d = make()
+        for _ in range(warmup):
+            d.process(host)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = d.process(host)
+        dt = time.perf_counter() - t0
+        rates[name] = (round(S * n * steps / dt / 1e6, 2), round(dt / steps * 1e3, 3))
+        rows[name] = out[:2]
+        d.close()
+    a, b = rows["one_handle"], rows["group_2x_same_gpu"]
+    bad = sum(1 for s in range(S) if int(a[1][s]) != int(b[1][s]) or
+              not np.array_equal(a[0][s, : (int(a[1][s]) + 7) // 8], b[0][s, : (int(b[1][s]) + 7) // 8]))
+    best = max(rates, key=lambda k: rates[k][0])
+    return {"kind": "drop_in", "value": rates[best][0], "unit": "MSa/s", "ms_per_step": rates[best][1],
+            "steps": steps, "warmup": warmup,
+            "config": {"workload": f"C2 from pageable host memory: {S} streams x 2^20 samples per synchronous "
+                                   f"call (BatchDeModulator); value = {best}"},
+            "one_handle": rates["one_handle"][0], "group_2x_same_gpu": rates["group_2x_same_gpu"][0],
+            "parity": {"group_vs_one_handle": {"streams": S, "mismatching": bad}},
+            "note": "PCIe-inclusive; [MSa/s, ms per call] per path in one_handle / group_2x_same_gpu"}
+
+
 def host_ring_c3_leg(dev, chunk=1 << 18, steps=2, warmup=1):
     """C3 fed from host memory through the pinned ring (qpsk_rx_*, the
     ModDemodOverSDR.cs:116-183 receive loop at batch scale): 4096 streams x
@@ -1116,7 +1159,8 @@ def compact_record(out, detail_name):
         s["workload"] = r.get("config", {}).get("workload")
         if r.get("kind") == "drop_in":
             # the drop-in's own shapes (host memory): their few fields as they are
-            s.update({k: r[k] for k in ("unit", "cpu_single_core", "h2d_GBps", "parity", "error") if k in r})
+            s.update({k: r[k] for k in ("unit", "cpu_single_core", "h2d_GBps", "one_handle", "group_2x_same_gpu",
+                                        "parity", "error") if k in r})
         else:
             s.update(_compact_body(r))
         subs[key] = s
@@ -1252,7 +1296,8 @@ def main():
     if world == 1 and not args.no_drop_in:
         # the drop-in's own shapes, host memory in: one stream
         # per handle, and C3 through the pinned ring.  PCIe-inclusive, never `value`
-        for key, leg in (("s1_host", s1_host_leg), ("host_ring_c3", host_ring_c3_leg)):
+        for key, leg in (("s1_host", s1_host_leg), ("batch_host_c2", batch_host_leg),
+                         ("host_ring_c3", host_ring_c3_leg)):
             try:
                 sub[key] = leg(dev)
             except Exception as e:       # a failed side leg must not cost the headline line
