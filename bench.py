@@ -705,6 +705,7 @@ def framer_pass(bits, nbits, S, stream, reps=5):
     del fr
     return {"tsc_ms": round(t_tsc / reps, 4), "framer_ms": round(t_push / reps, 4),
             "frames_per_call": round(frames / reps, 1),
+            "frames_per_s": round(frames / (t_push * 1e-3), 1) if t_push > 0 else None,
             "bits_GBps": round(row_bytes / (t_push / reps * 1e-3) / 1e9, 1) if t_push > 0 else None}
 
 
@@ -1044,7 +1045,7 @@ def run_config(key, args, rank, world, dev, steps, warmup, headline):
     }
     if rec.get("cpu_baseline") is None:
         rec["cpu_baseline"] = None
-    if headline and world == 1 and not args.no_framer and not args.timed_only:
+    if (headline or key == "c2") and world == 1 and not args.no_framer and not args.timed_only:
         rec["framer"] = framer_pass(bits, nbits, S, stream)
     if world == 1 and not args.no_host_ring and not args.timed_only and S * n * 8 <= (4 << 30):
         rec["host_ring"] = host_ring_pass(demod, iq, S, n)

@@ -16,8 +16,12 @@
 //   end search   RingIndexOf from count - (appended + |end|) (:133-149, :246)
 //   copy-out     RingCopyOut + ResetFramer (:151-167)
 //
-// Work per call is O(bits) with no serial walk; the framer moves ~2 bits per
-// symbol of traffic, noise next to the demod chain's 8 B/sample.
+// Work per call is O(bits) with no serial walk, and the scans stop at the
+// first match (the chunk holding it): on real traffic the start and end
+// markers sit near the start of a call's bits, and a frame that closes in the
+// call never writes its bytes to the ring (its payload is copied straight from
+// the bits).  The framer moves ~2 bits per symbol of traffic, noise next to
+// the demod chain's 8 B/sample.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -87,7 +91,32 @@ __device__ inline uint64_t load_be64(const uint8_t *row, int64_t b, int64_t nbyt
     return w;
 }
 
-// Candidate bit q of a hunt: carry bits, then the row from bit off0.
+// 64 bits from byte b on (MSB-first) of a 4-byte aligned buffer holding at
+// least b + 8 bytes: two dword loads and a byte swap instead of 8 byte loads
+__device__ inline uint64_t load_be64_aligned(const uint8_t *buf, int64_t b) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(buf + b);
+    return (static_cast<uint64_t>(__builtin_bswap32(w[0])) << 32) | __builtin_bswap32(w[1]);
+}
+
+// 64 bits from byte b on (MSB-first) of a row at any alignment whose valid
+// bytes end at nbytes (bytes past it read as 0).  Windows whose 12 bytes lie
+// inside the row take three aligned dword loads and a funnel shift; the rest
+// (the row's last bytes) go byte by byte, so nothing past the row is read.
+__device__ inline uint64_t load_be64_any(const uint8_t *row, int64_t b, int64_t nbytes) {
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(row + b);
+    const int m = static_cast<int>(addr & 3);
+    if (b + 12 <= nbytes) {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(addr - m);
+        const uint64_t lo = static_cast<uint64_t>(w[0]) | (static_cast<uint64_t>(w[1]) << 32);
+        const uint64_t hi = w[2];
+        // little-endian bytes m .. m+7 of the 12 loaded
+        const uint64_t v = m ? (lo >> (8 * m)) | (hi << (64 - 8 * m)) : lo;
+        return __builtin_bswap64(v);
+    }
+    return load_be64(row, b, nbytes);
+}
+
+// The candidate bit string of a hunt: carry bits, then the row from bit off0.
 struct Cand {
     const uint8_t *carry;
     int64_t ncarry;
@@ -95,6 +124,14 @@ struct Cand {
     int64_t off0;
     __device__ uint32_t bit(int64_t q) const {
         return q < ncarry ? bit_at(carry, q) : bit_at(row, off0 + q - ncarry);
+    }
+    // bits [q, q + 8) (q + 8 <= the string's length)
+    __device__ uint32_t bits8_at(int64_t q) const {
+        if (q >= ncarry) return bits8(row, off0 + q - ncarry);
+        if (q + 8 <= ncarry) return bits8(carry, q);
+        uint32_t v = 0;
+        for (int i = 0; i < 8; ++i) v = (v << 1) | bit(q + i);
+        return v;
     }
     // byte j of the candidate string (bits 8j..8j+7, zero past n)
     __device__ uint32_t byte(int64_t j, int64_t n) const {
@@ -116,25 +153,14 @@ __device__ void reset_state(FrState &s) {   // ResetFramer (:159-167)
     s.carry_bits = 0;
 }
 
-// First i in [from, count - n_pat] with ring[i .. i+n_pat) == pat, or -1
-// (RingIndexOf, :133-149).  Whole workgroup; result uniform.
-__device__ int64_t ring_index_of(const uint8_t *ring, int64_t count, const uint8_t *pat, int n_pat,
-                                 int64_t from, unsigned long long *best) {
-    if (threadIdx.x == 0) *best = ULLONG_MAX;
-    __syncthreads();
-    const int64_t last = count - n_pat;
-    const uint32_t p0 = pat[0];
-    for (int64_t i = from + threadIdx.x; i <= last; i += kFrThreads) {
-        if (ring[i] != p0) continue;
-        int k = 1;
-        while (k < n_pat && ring[i + k] == pat[k]) ++k;
-        if (k == n_pat) atomicMin(best, static_cast<unsigned long long>(i));
-    }
-    __syncthreads();
-    const unsigned long long b = *best;
-    __syncthreads();
-    return b == ULLONG_MAX ? -1 : static_cast<int64_t>(b);
-}
+// Positions a hunt / search chunk covers before the workgroup looks at its
+// result: the reference's scans stop at the first match (IndexOf,
+// RingIndexOf), and on real traffic that sits near the start of the row, so
+// the chunks run in ascending position order and stop as soon as the answer
+// cannot change.  (Until round 6 every position of the row was scanned and
+// the whole row copied into the candidate scratch and the ring first.)
+constexpr int kHuntWindows = kFrThreads;        // 32 positions each: 1 KB of candidate bits
+constexpr int kEndPerThread = 8;                // ring positions per thread and chunk
 
 __global__ void __launch_bounds__(kFrThreads) framer_push_kernel(FrArgs a) {
     __shared__ unsigned long long best[8];
@@ -149,44 +175,74 @@ __global__ void __launch_bounds__(kFrThreads) framer_push_kernel(FrArgs a) {
     const uint8_t *row = a.bits + s * a.bits_stride;
     uint8_t *ring = a.ring + s * a.ring_cap;
     FrState st = a.st[s];
-    int64_t appended = 0;
     __syncthreads();                       // every wave holds st before thread 0 may rewrite it
+
+    // the bytes this call appends to the ring, as a function (materialised only
+    // when the frame stays open past this call): case A = candidate bits from
+    // the end of the start marker, case B = the packer's partial byte + rxBits
+    bool entering = false;                 // case A (the frame opens in this call)
+    Cand src{nullptr, 0, row, off0};
+    int64_t mend = 0;                      // case A: first candidate bit after the start marker
+    const int P = st.pack_bits;            // case B
+    const uint32_t pack_byte = static_cast<uint32_t>(st.pack_byte);
+    int64_t produced = 0;
+    int rem = 0;
 
     if (!st.in_frame) {
         // ---- 1) start hunt over carry + rxBits (:183-236) ----
+        // BitsToBytes(cand, off) + IndexOf for off = 0..7 == the first bit
+        // position q of the marker pattern with the smallest q mod 8; every
+        // thread tests 32 positions of one 64-bit window per chunk
         uint8_t *carry = a.carry + s * a.carry_stride;
         uint8_t *cand = a.scratch + s * a.scr_stride;
-        const Cand src{carry, st.carry_bits, row, off0};
+        src.carry = carry;
+        src.ncarry = st.carry_bits;
         const int64_t nc = st.carry_bits + nb;
         const int64_t ncb = (nc + 7) >> 3;
-        for (int64_t j = tid; j < ncb; j += kFrThreads) cand[j] = static_cast<uint8_t>(src.byte(j, nc));
+        const int64_t pad_end = ncb + 8;                 // zero bytes behind the string (scratch slack)
         if (tid < 8) best[tid] = ULLONG_MAX;
-        __syncthreads();
-
         const int64_t limit = nc - 8 * static_cast<int64_t>(a.ns);   // last start position
         const uint32_t m0 = a.start[0];
-        for (int64_t w = tid; 32 * w <= limit; w += kFrThreads) {
-            const uint64_t win = load_be64(cand, 4 * w, ncb);
-            const int jmax = static_cast<int>(limit - 32 * w < 31 ? limit - 32 * w : 31);
-            for (int j = 0; j <= jmax; ++j) {
-                if (((win >> (56 - j)) & 0xffu) != m0) continue;
-                const int64_t q = 32 * w + j;
-                int k = 1;
-                while (k < a.ns && bits8(cand, q + 8 * k) == a.start[k]) ++k;
-                if (k == a.ns) atomicMin(&best[j & 7], static_cast<unsigned long long>(q));
+        int64_t mat = 0;                                 // candidate bytes [0, mat) are in the scratch
+        for (int64_t w0 = 0; 32 * w0 <= limit; w0 += kHuntWindows) {
+            // the chunk's windows read bytes < 4 (w0 + kHuntWindows) + 8, the
+            // marker checks up to ns + 1 bytes beyond
+            int64_t need = 4 * (w0 + kHuntWindows) + 8 + a.ns + 1;
+            need = need < pad_end ? need : pad_end;
+            for (int64_t j = mat + tid; j < need; j += kFrThreads)
+                cand[j] = static_cast<uint8_t>(j < ncb ? src.byte(j, nc) : 0u);
+            mat = need > mat ? need : mat;
+            __syncthreads();
+            const int64_t w = w0 + tid;
+            if (32 * w <= limit) {
+                const uint64_t win = load_be64_aligned(cand, 4 * w);
+                const int jmax = static_cast<int>(limit - 32 * w < 31 ? limit - 32 * w : 31);
+                for (int j = 0; j <= jmax; ++j) {
+                    if (((win >> (56 - j)) & 0xffu) != m0) continue;
+                    const int64_t q = 32 * w + j;
+                    int k = 1;
+                    while (k < a.ns && bits8(cand, q + 8 * k) == a.start[k]) ++k;
+                    if (k == a.ns) atomicMin(&best[j & 7], static_cast<unsigned long long>(q));
+                }
             }
+            __syncthreads();
+            // offset 0 matched: no later chunk can hold a smaller offset-0
+            // position, and offset 0 wins over every other offset
+            if (best[0] != ULLONG_MAX) break;
         }
-        __syncthreads();
         int64_t q = -1;
         int off = -1;
         for (int o = 0; o < 8; ++o)
             if (best[o] != ULLONG_MAX) { q = static_cast<int64_t>(best[o]); off = o; break; }
 
         if (q < 0) {
-            // no start: keep min(|cand|, 8|start|+7) tail bits (:233-235)
+            // no start: keep min(|cand|, 8|start|+7) tail bits (:233-235),
+            // copied from the scratch (the carry is rewritten in place)
+            for (int64_t j = mat + tid; j < pad_end; j += kFrThreads)
+                cand[j] = static_cast<uint8_t>(j < ncb ? src.byte(j, nc) : 0u);
+            __syncthreads();
             const int64_t keep = nc < 8 * static_cast<int64_t>(a.ns) + 7 ? nc : 8 * static_cast<int64_t>(a.ns) + 7;
             const int64_t base = nc - keep;
-            __syncthreads();                                 // carry was read into cand above
             for (int64_t j = tid; j < (keep + 7) >> 3; j += kFrThreads) {
                 const int64_t p = base + 8 * j;
                 uint32_t v;
@@ -204,9 +260,9 @@ __global__ void __launch_bounds__(kFrThreads) framer_push_kernel(FrArgs a) {
             return;
         }
         // enter the frame: ring cleared, payload = cand bits after the marker (:203-214)
-        const int64_t mend = q + 8 * static_cast<int64_t>(a.ns);
+        mend = q + 8 * static_cast<int64_t>(a.ns);
         const int64_t len = nc - mend;
-        const int64_t produced = len >> 3;
+        produced = len >> 3;
         if (produced > a.ring_cap) {                         // overflow -> drop + resync (:215-220)
             if (tid == 0) {
                 reset_state(st);
@@ -214,22 +270,19 @@ __global__ void __launch_bounds__(kFrThreads) framer_push_kernel(FrArgs a) {
             }
             return;
         }
-        for (int64_t i = tid; i < produced; i += kFrThreads)
-            ring[i] = static_cast<uint8_t>(bits8(cand, mend + 8 * i));
+        entering = true;
         st.in_frame = 1;
         st.locked_off = off;
-        st.count = produced;
-        const int rem = static_cast<int>(len & 7);
+        rem = static_cast<int>(len & 7);
         uint32_t pb = 0;
-        for (int r = 0; r < rem; ++r) pb = (pb << 1) | bit_at(cand, mend + 8 * produced + r);
+        for (int r = 0; r < rem; ++r) pb = (pb << 1) | src.bit(mend + 8 * produced + r);
         st.pack_byte = static_cast<int32_t>(pb);
         st.pack_bits = rem;
-        appended = produced;
+        st.count = 0;                                        // the ring restarts (RingClear)
     } else {
         // ---- 2) inside a frame: pack rxBits behind the partial byte (:238-246) ----
-        const int P = st.pack_bits;
         const int64_t total = P + nb;
-        const int64_t produced = total >> 3;
+        produced = total >> 3;
         if (st.count + produced > a.ring_cap) {
             if (tid == 0) {
                 reset_state(st);
@@ -237,39 +290,57 @@ __global__ void __launch_bounds__(kFrThreads) framer_push_kernel(FrArgs a) {
             }
             return;
         }
-        uint8_t *dst = ring + st.count;
-        for (int64_t j = tid; j < produced; j += kFrThreads) {
-            uint32_t v;
-            if (j == 0 && P > 0) {
-                v = static_cast<uint32_t>(st.pack_byte);
-                for (int i = 0; i < 8 - P; ++i) v = (v << 1) | bit_at(row, off0 + i);
-            } else {
-                v = bits8(row, off0 + 8 * j - P);
-            }
-            dst[j] = static_cast<uint8_t>(v);
-        }
         // leftover bits: W[8*produced, total) of W = pack prefix + rxBits
-        const int rem = static_cast<int>(total & 7);
+        rem = static_cast<int>(total & 7);
         uint32_t pb = 0;
         for (int r = 0; r < rem; ++r) {
             const int64_t w = 8 * produced + r;
-            pb = (pb << 1) | (w < P ? (static_cast<uint32_t>(st.pack_byte) >> (P - 1 - w)) & 1u
-                                    : bit_at(row, off0 + w - P));
+            pb = (pb << 1) | (w < P ? (pack_byte >> (P - 1 - w)) & 1u : bit_at(row, off0 + w - P));
         }
         st.pack_byte = static_cast<int32_t>(pb);
         st.pack_bits = rem;
-        st.count += produced;
-        appended = produced;
     }
-    __syncthreads();                                         // ring bytes visible to the WG
+    const int64_t old_count = st.count;
+    const int64_t count = old_count + produced;
+    // byte j of this call's appended bytes (j < produced)
+    auto newbyte = [&](int64_t j) -> uint32_t {
+        if (entering) return src.bits8_at(mend + 8 * j);
+        if (j == 0 && P > 0) {
+            uint32_t v = pack_byte;
+            for (int i = 0; i < 8 - P; ++i) v = (v << 1) | bit_at(row, off0 + i);
+            return v & 0xffu;
+        }
+        return bits8(row, off0 + 8 * j - P);
+    };
+    // ring byte i after the append (i < count), without writing the ring
+    auto ring_byte = [&](int64_t i) -> uint32_t { return i < old_count ? ring[i] : newbyte(i - old_count); };
 
-    const int64_t from = st.count - (appended + a.ne) > 0 ? st.count - (appended + a.ne) : 0;
-    const int64_t end_at = ring_index_of(ring, st.count, a.end, a.ne, from, &best_end);
+    // ---- 3) end search: RingIndexOf from count - (appended + |end|) (:133-149, :246)
+    const int64_t from = count - (produced + a.ne) > 0 ? count - (produced + a.ne) : 0;
+    const int64_t last = count - a.ne;                       // last start position of the end marker
+    if (tid == 0) best_end = ULLONG_MAX;
+    __syncthreads();
+    const uint32_t e0 = a.end[0];
+    for (int64_t c0 = from; c0 <= last; c0 += kFrThreads * kEndPerThread) {
+#pragma unroll
+        for (int k = 0; k < kEndPerThread; ++k) {
+            const int64_t i = c0 + k * kFrThreads + tid;
+            if (i > last || ring_byte(i) != e0) continue;
+            int m = 1;
+            while (m < a.ne && ring_byte(i + m) == a.end[m]) ++m;
+            if (m == a.ne) atomicMin(&best_end, static_cast<unsigned long long>(i));
+        }
+        __syncthreads();
+        if (best_end != ULLONG_MAX) break;                   // the first occurrence is in this chunk
+    }
+    const int64_t end_at = best_end == ULLONG_MAX ? -1 : static_cast<int64_t>(best_end);
     if (end_at >= 0) {                                       // RingCopyOut + ResetFramer (:223-226)
+        // the frame closes: its payload comes straight from the ring and this
+        // call's bits; the appended bytes never need to be stored
         uint8_t *out = a.payload ? a.payload + s * a.payload_stride : nullptr;
         const int64_t n = end_at < a.payload_stride ? end_at : a.payload_stride;
         if (out)
-            for (int64_t i = tid; i < n; i += kFrThreads) out[i] = ring[i];
+            for (int64_t i = tid; i < n; i += kFrThreads) out[i] = static_cast<uint8_t>(ring_byte(i));
         if (tid == 0) {
             a.n_payload[s] = end_at;
             reset_state(st);
@@ -277,7 +348,12 @@ __global__ void __launch_bounds__(kFrThreads) framer_push_kernel(FrArgs a) {
         }
         return;
     }
-    if (tid == 0) a.st[s] = st;
+    // the frame stays open: the appended bytes go into the ring (AppendBitsToRing)
+    for (int64_t j = tid; j < produced; j += kFrThreads) ring[old_count + j] = static_cast<uint8_t>(newbyte(j));
+    if (tid == 0) {
+        st.count = count;
+        a.st[s] = st;
+    }
 }
 
 // Pattern bits ride by value in the kernel arguments up to 4096 bits (the
@@ -288,7 +364,9 @@ struct TscPat {
 
 // rx.IndexOf(tsc, Ordinal) per stream (:413-422).  Each thread tests 32
 // positions against the first min(m, 32) pattern bits from one 64-bit window,
-// the rest bit by bit; the minimum position reduces in LDS.
+// the rest bit by bit; the minimum position reduces in LDS.  Chunks of
+// kFrThreads windows run in ascending position order and the search stops
+// after the chunk holding the first match.
 __global__ void __launch_bounds__(kFrThreads)
 tsc_find_kernel(const uint8_t *bits, int64_t stride, const int64_t *n_bits, TscPat small,
                 const uint8_t *big, int32_t m, int64_t *offsets) {
@@ -305,21 +383,25 @@ tsc_find_kernel(const uint8_t *bits, int64_t stride, const int64_t *n_bits, TscP
     const uint64_t kmask = km == 32 ? 0xffffffffull : ((1ull << km) - 1);
     if (threadIdx.x == 0) best = ULLONG_MAX;
     __syncthreads();
-    for (int64_t w = threadIdx.x; 32 * w <= limit; w += kFrThreads) {
-        const uint64_t win = load_be64(row, 4 * w, nbytes);
-        const int jmax = static_cast<int>(limit - 32 * w < 31 ? limit - 32 * w : 31);
-        for (int j = 0; j <= jmax; ++j) {
-            if (((win >> (64 - km - j)) & kmask) != key) continue;
-            const int64_t q = 32 * w + j;
-            int k = km;
-            while (k < m && bit_at(row, q + k) == bit_at(pat, k)) ++k;
-            if (k == m) {
-                atomicMin(&best, static_cast<unsigned long long>(q));
-                break;                                       // later j of this window are larger
+    for (int64_t w0 = 0; 32 * w0 <= limit; w0 += kFrThreads) {
+        const int64_t w = w0 + threadIdx.x;
+        if (32 * w <= limit) {
+            const uint64_t win = load_be64_any(row, 4 * w, nbytes);
+            const int jmax = static_cast<int>(limit - 32 * w < 31 ? limit - 32 * w : 31);
+            for (int j = 0; j <= jmax; ++j) {
+                if (((win >> (64 - km - j)) & kmask) != key) continue;
+                const int64_t q = 32 * w + j;
+                int k = km;
+                while (k < m && bit_at(row, q + k) == bit_at(pat, k)) ++k;
+                if (k == m) {
+                    atomicMin(&best, static_cast<unsigned long long>(q));
+                    break;                                   // later j of this window are larger
+                }
             }
         }
+        __syncthreads();
+        if (best != ULLONG_MAX) break;                       // no later chunk holds a smaller one
     }
-    __syncthreads();
     if (threadIdx.x == 0) offsets[s] = best == ULLONG_MAX ? -1 : static_cast<int64_t>(best) + m;
 }
 

@@ -30,7 +30,7 @@ for step in "$@"; do
     bench)
       a=${arg//,/ }; [ -z "$a" ] && a="--steps 20 --warmup 5"
       n=$(ls "$O" | grep -c '^bench' || true)
-      timeout -k 10 600 python bench.py $a > "$O/bench$n.json" 2> "$O/bench$n.err" \
+      timeout -k 10 600 python bench.py $a --detail "$O/bench${n}_detail.json" > "$O/bench$n.json" 2> "$O/bench$n.err" \
         || { tail -20 "$O/bench$n.err"; exit 1; }
       echo "bench$n done: $a" ;;
     prof)
