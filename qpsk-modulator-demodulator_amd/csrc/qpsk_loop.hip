@@ -82,12 +82,28 @@ constexpr int kCap256Sps8 = 51;
 constexpr int kCap512Sps8 = 100;
 typedef double d2 __attribute__((ext_vector_type(2)));
 
-// M&M -> Costas symbol slots hold doubles: the M&M wave has them widened
-// already.  Float slots (21 KB less LDS) measured slower, the two widenings
-// landing on the Costas wave (C3 loop 45.6 vs 47.6 ms, round 2)
+// M&M -> Costas symbol slots.  64-sample rounds (the 32 x 64 shapes of C3, C4
+// and C5): the M&M's float symbols, which the Costas wave widens (exactly);
+// the M&M's store halves (ds_write_b64), and with the M&M pacing these shapes
+// the loop runs faster: C3 331.7 -> 318.0 and C4 396.9 -> 377.5 cycles per
+// symbol, A/B x2 on one MI355X (profiles/r06_float_slots_ab.txt).  Longer
+// rounds (C2's 6 x 512, 12 x 256, 24 x 128), where the Costas wave paces and
+// the two widenings land on it: the doubles the M&M already has (C2 274 ->
+// 291 with float slots).  Round 2 measured float slots slower at C3 when the
+// Costas wave still paced there.
 typedef d2 sym_t;
-__device__ __forceinline__ sym_t to_sym(float, float, double cid, double cqd) { return d2{cid, cqd}; }
 __device__ __forceinline__ d2 from_sym(d2 v) { return v; }
+__device__ __forceinline__ d2 from_sym(f2 v) { return d2{static_cast<double>(v.x), static_cast<double>(v.y)}; }
+template <typename S> struct SymPut;
+template <> struct SymPut<d2> {
+    __device__ static d2 put(float, float, double cid, double cqd) { return d2{cid, cqd}; }
+};
+template <> struct SymPut<f2> {
+    __device__ static f2 put(float ci, float cq, double, double) { return f2{ci, cq}; }
+};
+// (the glibc-trig Costas step paces its loop at every shape: doubles there)
+template <int KB, int TRIG>
+using SymSlot = typename std::conditional<KB == 64 && TRIG == 0, f2, d2>::type;
 
 __device__ __forceinline__ int wave_max_i32(int v) {
 #pragma unroll
@@ -164,7 +180,7 @@ struct LoopLds {
     // immediate offset is 16 bits, so the Costas wave's per-step slot reads and
     // writes then fold their constant part into the instruction instead of one
     // v_add_u32 each (behind the 66 KB ring they did)
-    sym_t sym[2 * SPW * RS];       // M&M -> Costas [slot][stream][RS] (see sym_t)
+    SymSlot<KB, TRIG> sym[2 * SPW * RS];   // M&M -> Costas [slot][stream][RS] (see SymSlot)
     typename std::conditional<ROTB, uint16_t, f2>::type rot[2 * SPW * RS];   // Costas -> decode
     int cnt[4 * SPW + 4];          // symbols produced by the M&M in round r: cnt[r & 3];
                                    // cnt[4*SPW + (r & 3)] = their minimum over the batch
@@ -424,7 +440,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 row[2] = row[kMir + kRing - 2]; row[3] = row[kMir + kRing - 1];
             }
             const int rend = (r + 1) * KB < cnt ? (r + 1) * KB : cnt;
-            sym_t *out = L.sym + ((r & 1) * SPW + rowl) * L.RS;
+            auto *out = L.sym + ((r & 1) * SPW + rowl) * L.RS;
             int kmax = stop ? 0 : (cap - nsym < CAP ? cap - nsym : CAP);
             int k = 0, kuni = 0;
             lds_f2 *tp = (lds_f2 *)taps(base);
@@ -476,7 +492,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 interp(ci, cq);
                 has_prev = 1;
                 psid = ci; psqd = cq;
-                out[k++] = to_sym(ci, cq, psid, psqd);
+                out[k++] = SymPut<SymSlot<KB, TRIG>>::put(ci, cq, psid, psqd);
                 psi = ci; psq = cq;
                 pdid = ci >= 0.0f ? 1.0 : -1.0;
                 pdqd = cq >= 0.0f ? 1.0 : -1.0;
@@ -505,7 +521,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
                 pdid = did; pdqd = dqd;
                 advance(sps + corr, load);
                 // stored after the next taps' loads (LDS serves in issue order)
-                out[k++] = to_sym(ci, cq, cid, cqd);
+                out[k++] = SymPut<SymSlot<KB, TRIG>>::put(ci, cq, cid, cqd);
 #ifdef QPSK_LOOP_STAMPS
                 ++c_iters;
 #endif
@@ -704,7 +720,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             if (cl >= ACT) continue;   // exec = the batch's lanes for the whole round
             const int crow = cl < SPW ? cl : 0;
             const int m = cmine ? L.cnt[((r - 1) & 3) * SPW + crow] : 0;
-            const sym_t *in = L.sym + (slot * SPW + crow) * L.RS;
+            const auto *in = L.sym + (slot * SPW + crow) * L.RS;
             // (TRIG 1: both lanes of a stream store the same value to the same slot)
             auto *out = L.rot + (slot * SPW + crow) * L.RS;
             d2 y;
@@ -716,7 +732,7 @@ __global__ __launch_bounds__(256) void loop_kernel(LoopArgs a, LoopParams P) {
             // fast path for ~10^5 calls (profiles/archive/r02_state_c3.log: a 4096-stream
             // C3 batch has 27 such streams after 6 calls; with the old 1e6 range
             // their 26 workgroups redid every round and the kernel took 2.7x)
-            auto widen = [](sym_t v) { return from_sym(v); };
+            auto widen = [](SymSlot<KB, TRIG> v) { return from_sym(v); };
             // the previous step's decisions, stored under this step's table loads
             // (row entry CAP, past the round's symbols, takes the first store)
             typename std::remove_reference<decltype(out[0])>::type pend{};
