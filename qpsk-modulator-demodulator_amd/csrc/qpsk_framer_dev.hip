@@ -388,14 +388,42 @@ tsc_find_kernel(const uint8_t *bits, int64_t stride, const int64_t *n_bits, TscP
         if (32 * w <= limit) {
             const uint64_t win = load_be64_any(row, 4 * w, nbytes);
             const int jmax = static_cast<int>(limit - 32 * w < 31 ? limit - 32 * w : 31);
-            for (int j = 0; j <= jmax; ++j) {
-                if (((win >> (64 - km - j)) & kmask) != key) continue;
+            // position j of the window matches the first km pattern bits
+            auto full = [&](int j) -> bool {
+                if (j > jmax || ((win >> (64 - km - j)) & kmask) != key) return false;
                 const int64_t q = 32 * w + j;
                 int k = km;
                 while (k < m && bit_at(row, q + k) == bit_at(pat, k)) ++k;
-                if (k == m) {
-                    atomicMin(&best, static_cast<unsigned long long>(q));
-                    break;                                   // later j of this window are larger
+                return k == m;
+            };
+            if (m >= 16) {
+                // a 16-bit prefix filter on two positions per 32-bit word: the
+                // word of bits [o, o + 32) holds the 16-bit values at o (high
+                // half) and o + 16 (low half), so 16 funnel shifts cover the
+                // window's 32 positions; a half equal to the prefix (haszero on
+                // the XOR, false positives possible, never false negatives) is
+                // checked in full.  ~5 ops per two positions instead of ~6 per one
+                const uint32_t k16 = key >> (km - 16);
+                const uint32_t kk = (k16 << 16) | k16;
+                const uint32_t whi = static_cast<uint32_t>(win >> 32), wlo = static_cast<uint32_t>(win);
+                int first = 64;
+#pragma unroll
+                for (int o = 0; o < 16; ++o) {
+                    const uint32_t x = o ? (whi << o) | (wlo >> (32 - o)) : whi;
+                    const uint32_t z = x ^ kk;
+                    const uint32_t hz = (z - 0x00010001u) & ~z & 0x80008000u;
+                    if (__builtin_expect(hz != 0, 0)) {
+                        if ((hz & 0x80000000u) && o < first && full(o)) first = o;
+                        if ((hz & 0x00008000u) && o + 16 < first && full(o + 16)) first = o + 16;
+                    }
+                }
+                if (first < 64) atomicMin(&best, static_cast<unsigned long long>(32 * w + first));
+            } else {
+                for (int j = 0; j <= jmax; ++j) {
+                    if (full(j)) {
+                        atomicMin(&best, static_cast<unsigned long long>(32 * w + j));
+                        break;                               // later j of this window are larger
+                    }
                 }
             }
         }

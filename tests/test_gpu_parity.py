@@ -565,10 +565,11 @@ def test_host_ring_errors():
 
 
 def test_c_abi_demo_from_plain_c():
-    """The boundary from plain C, the way a cgo / JNI / P/Invoke binding calls it:
-    tools/c_abi_demo (built by build()) demodulates ragged calls through
-    qpsk_demod_process and the qpsk_rx ring and checks every call's bits against
-    the oracle's DeModulate."""
+    """The boundary from plain C, the way a cgo / JNI / P/Invoke binding (or a
+    C++ multi-GPU driver) calls it: tools/c_abi_demo (built by build())
+    demodulates ragged calls through qpsk_demod_process, the qpsk_rx ring and a
+    two-shard qpsk_demod_group on device 0, and checks every call's bits
+    against the oracle's DeModulate."""
     import os
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -576,7 +577,7 @@ def test_c_abi_demo_from_plain_c():
     assert os.path.exists(exe), "run __graft_entry__.build() (make -f tools/c_abi_demo.mk)"
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "bits identical to the oracle" in r.stdout
+    assert "bits identical to the oracle" in r.stdout and "2-shard group" in r.stdout
 
 
 @pytest.mark.parametrize("layout", ["direct", "staged"])

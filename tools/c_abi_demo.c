@@ -3,8 +3,11 @@
  * no HIP headers): what a cgo / JNI / P/Invoke binding of include/qpsk_demod.h
  * does.  S streams of differential QPSK (oracle modulator, testAtDataLevel-like
  * sps 8 / 65 taps / alpha 0.4, each stream with its own LO pair) go through
- *   1. qpsk_demod_process on host memory, in ragged chunks, and
- *   2. the host-fed ring (qpsk_rx_*) on a second handle,
+ *   1. qpsk_demod_process on host memory, in ragged chunks,
+ *   2. the host-fed ring (qpsk_rx_*) on a second handle, and
+ *   3. a multi-GPU group (qpsk_demod_group_*: the C++ multi-GPU driver's
+ *      entry) over the devices in QPSK_DEMO_DEVICES
+ *      (comma list, default "0,0": two shards on device 0),
  * and every call's bits must equal the oracle's DeModulate on the same chunk
  * (or_demod_demodulate_ex, QPSKDeModulator.cs:345-410; test infrastructure).
  * Exit status 0 = identical.  Built by tools/c_abi_demo.mk (build());
@@ -95,12 +98,33 @@ int main(void) {
     check(qpsk_demod_create(&p, S, &h2), "create (ring)");
     qpsk_rx *ring;
     check(qpsk_rx_create(h2, 2, &ring), "rx_create");
+    int32_t devs[8];
+    int n_dev = 0;
+    {
+        const char *e = getenv("QPSK_DEMO_DEVICES");
+        char buf[64];
+        snprintf(buf, sizeof buf, "%s", e && *e ? e : "0,0");
+        for (char *t = strtok(buf, ","); t && n_dev < 8; t = strtok(NULL, ",")) devs[n_dev++] = atoi(t);
+    }
+    qpsk_demod_group *grp;
+    check(qpsk_demod_group_create(&p, devs, n_dev, S, &grp), "group_create");
+    for (int k = 0; k < n_dev; ++k) {
+        int32_t f, c, d;
+        check(qpsk_demod_group_shard(grp, k, &f, &c, &d, NULL), "group_shard");
+        int32_t f2, c2;
+        check(qpsk_shard_streams(S, n_dev, k, &f2, &c2), "shard_streams");
+        if (f != f2 || c != c2 || d != devs[k]) {
+            fprintf(stderr, "shard %d: [%d, +%d) on %d, expected [%d, +%d) on %d\n", k, f, c, d, f2, c2, devs[k]);
+            return 1;
+        }
+    }
 
     const int64_t stride = 2 * n_call_max;
     const int64_t bstride = (2 * qpsk_demod_max_symbols(h, n_call_max) + 7) / 8 + 8;
     float *iq = calloc((size_t)S * stride, sizeof(float));
     uint8_t *bits = calloc((size_t)S * bstride, 1), *bits2 = calloc((size_t)S * bstride, 1);
-    int64_t nb[S], nb2[S];
+    uint8_t *bits3 = calloc((size_t)S * bstride, 1);
+    int64_t nb[S], nb2[S], nb3[S];
     or_demod *ref[S];
     for (int s = 0; s < S; ++s) {
         or_demod_cfg cfg;
@@ -120,6 +144,8 @@ int main(void) {
                                  NULL, 0, NULL), "process");
         check(qpsk_rx_submit(ring, iq, stride, 0, len[c], NULL), "rx_submit");
         check(qpsk_rx_collect(ring, bits2, bstride, nb2, NULL), "rx_collect");
+        check(qpsk_demod_group_process(grp, QPSK_MODE_DEMODULATE, iq, stride, 0, len[c], QPSK_MEM_HOST, bits3,
+                                       bstride, nb3, NULL, 0, NULL), "group_process");
         for (int s = 0; s < S; ++s) {
             long nsy = 0, tsc = 0;
             const long nr = or_demod_demodulate_ex(ref[s], sig[s] + 2 * pos[c][s], 2 * len[c][s], rb,
@@ -132,17 +158,22 @@ int main(void) {
                 fprintf(stderr, "call %d stream %d: ring bits differ (%lld vs %ld)\n", c, s, (long long)nb2[s], nr);
                 bad = 1;
             }
+            if (!same_bits(bits3 + s * bstride, nb3[s], rb, nr)) {
+                fprintf(stderr, "call %d stream %d: group bits differ (%lld vs %ld)\n", c, s, (long long)nb3[s], nr);
+                bad = 1;
+            }
         }
     }
     check(qpsk_rx_destroy(ring), "rx_destroy");
+    check(qpsk_demod_group_destroy(grp), "group_destroy");
     check(qpsk_demod_destroy(h2), "destroy");
     check(qpsk_demod_destroy(h), "destroy");
     for (int s = 0; s < S; ++s) {
         or_demod_free(ref[s]);
         free(sig[s]);
     }
-    free(iq); free(bits); free(bits2); free(rb); free(rsym);
-    printf("c_abi_demo: %d streams x %d ragged calls (%lld samples), process() and qpsk_rx: %s\n", S, CALLS,
-           (long long)n_min, bad ? "MISMATCH" : "bits identical to the oracle");
+    free(iq); free(bits); free(bits2); free(bits3); free(rb); free(rsym);
+    printf("c_abi_demo: %d streams x %d ragged calls (%lld samples), process(), qpsk_rx and a %d-shard group: %s\n",
+           S, CALLS, (long long)n_min, n_dev, bad ? "MISMATCH" : "bits identical to the oracle");
     return bad;
 }
