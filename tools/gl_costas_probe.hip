@@ -25,6 +25,16 @@ __device__ __forceinline__ void swap_halves(double r, double *lower, double *upp
     *upper = __builtin_bit_cast(double, (static_cast<uint64_t>(ph[1]) << 32) | pl[1]);
 }
 
+// lanes 2l and 2l + 1 carry one stream: each gets its partner's value with one
+// quad_perm [1,0,3,2] DPP move per word
+__device__ __forceinline__ double pair_partner(double r) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, r);
+    const int lo = static_cast<int>(static_cast<uint32_t>(b)), hi = static_cast<int>(static_cast<uint32_t>(b >> 32));
+    const uint32_t plo = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(lo, lo, 0xB1, 0xF, 0xF, false));
+    const uint32_t phi = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(hi, hi, 0xB1, 0xF, 0xF, false));
+    return __builtin_bit_cast(double, (static_cast<uint64_t>(phi) << 32) | plo);
+}
+
 __device__ __forceinline__ double signsel(double x, bool pos) {
     const uint64_t b = __builtin_bit_cast(uint64_t, x);
     float h = __builtin_bit_cast(float, static_cast<uint32_t>(b >> 32));
@@ -176,7 +186,10 @@ __device__ __forceinline__ void fs_early(double x, const qpsk_gl_fs_lane *K, con
 // from registers, 3 no TAYLOR_SIN, 4 = 1+2+3, 5 cheap trig (no glibc code),
 // 6 the local copy of the step (check that it times like 0), 7 no prepare
 // (xa = |theta|, region A only), 8 = 7+2+3, 9 early row read, 10 = 9 +
-// region A merged into C, 11 the header's qpsk_gl_fs_pair (= 10)
+// region A merged into C, 11 the header's qpsk_gl_fs_pair (= 10), 12 = 11
+// without the hand-over, 13 = 11 with lanes 2l, 2l + 1 per stream and a DPP
+// hand-over whose selects fold into the swap, 14 = 13 with the hand-over
+// as explicit selects by lane parity (then fs_finish)
 template <int V>
 __global__ __launch_bounds__(64) void gl_costas(const d2 *sym_g, const double *tab_g, float *out_g, long long *cyc,
                                                 int reps) {
@@ -187,7 +200,8 @@ __global__ __launch_bounds__(64) void gl_costas(const d2 *sym_g, const double *t
     for (int i = lane; i < 110; i += 64) qpsk_gl_half_tables(tab_g, i, tab + 4 * i, tab + 440 + 4 * i);
     for (int i = lane; i < 32 * kRS; i += 64) sym[i] = sym_g[i];
     __syncthreads();
-    const int cl = lane & 31, half = lane >> 5;
+    constexpr bool PAIR = V == 13 || V == 14;
+    const int cl = PAIR ? lane >> 1 : lane & 31, half = PAIR ? lane & 1 : lane >> 5;
     const double *tabh = tab + (half ? 440 : 0);
     qpsk_gl_fs_lane KF = qpsk_gl_fs_lane_init(half == 0);
     asm volatile("" : "+v"(KF.L0), "+v"(KF.L1), "+v"(KF.hp1L), "+v"(KF.sgnm), "+v"(KF.tsh), "+v"(KF.sign));
@@ -209,6 +223,24 @@ __global__ __launch_bounds__(64) void gl_costas(const d2 *sym_g, const double *t
         if constexpr (V == 5) {
             cs = 1.0 - 0.5 * theta * theta;
             sn = theta;
+        } else if constexpr (V == 12) {
+            int sw;
+            const double rh = qpsk_gl_fs_pair(theta, &KF, tabh, &sw);
+            qpsk_gl_fs_finish(theta, sw, rh, rh, &KF, &sn, &cs);
+        } else if constexpr (V == 13) {
+            int sw;
+            const double rh = qpsk_gl_fs_pair(theta, &KF, tabh, &sw);
+            const double P = pair_partner(rh);
+            const int swp = sw ^ half;
+            const double s = swp ? P : rh;
+            cs = swp ? rh : P;
+            sn = qpsk_gl_with_hi(s, qpsk_gl_hi(s) ^ (qpsk_gl_hi(theta) & KF.sign));
+        } else if constexpr (V == 14) {
+            int sw;
+            const double rh = qpsk_gl_fs_pair(theta, &KF, tabh, &sw);
+            const double P = pair_partner(rh);
+            const double VS = half ? P : rh, VC = half ? rh : P;
+            qpsk_gl_fs_finish(theta, sw, VS, VC, &KF, &sn, &cs);
         } else if constexpr (V == 11) {
             int sw;
             const double rh = qpsk_gl_fs_pair(theta, &KF, tabh, &sw);
@@ -317,5 +349,8 @@ int main() {
     run<9>("early row read", sym, tab, out, cyc);
     run<10>("early row read, region A merged into C", sym, tab, out, cyc);
     run<11>("qpsk_gl_fs_pair (round-5 header)", sym, tab, out, cyc);
+    run<12>("fs_pair, no hand-over", sym, tab, out, cyc);
+    run<13>("fs_pair, lane pairs, DPP, folded selects", sym, tab, out, cyc);
+    run<14>("fs_pair, lane pairs, DPP, parity selects", sym, tab, out, cyc);
     return 0;
 }
