@@ -15,6 +15,10 @@
 //   V5  the TED without the decision doubles (e from the sums alone)
 //   V6  double symbol slot (ds_write_b128, the layout before round 6)
 //   V7  V3 + V1
+//   V8  V0 with ring rows of 262 float2 instead of 260 (2-way instead of
+//       4-way bank conflicts on the tap reads when all lanes sit at one position)
+//   V9  V0 with rows of 261 float2 (conflict-free; not 16-B aligned, bench only)
+//   V10 V0 with per-lane timing phases spread over the ring (random banks)
 // hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -mllvm -amdgpu-sched-strategy=max-ilp
 #include <hip/hip_runtime.h>
 
@@ -25,15 +29,17 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 typedef double d2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const f2 lds_f2;
 
-constexpr int kRing = 256, kRow = 4 + kRing, kRS = 29;
+constexpr int kRing = 256, kRS = 29;
+template <int V> constexpr int row_of() { return V == 8 ? 262 : (V == 9 ? 261 : 260); }
 
 template <int V>
 __global__ __launch_bounds__(64) void mm(const f2 *src, float *out_g, long long *cyc, int reps, double sps) {
-    __shared__ f2 ring[32 * kRow];
+    constexpr int kRow = row_of<V>();
+    __shared__ f2 ring[32 * 262];
     __shared__ f2 symf[32 * kRS];
     __shared__ d2 symd[32 * kRS];
     const int lane = threadIdx.x;
-    for (int i = lane; i < 32 * kRow; i += 64) ring[i] = src[i];
+    for (int i = lane; i < 32 * 262; i += 64) ring[i] = src[i];
     __syncthreads();
     if (lane >= 32) return;
     const double kp = 2.622462326512427e-3, ki = 3.443172085385801e-06;
@@ -51,7 +57,7 @@ __global__ __launch_bounds__(64) void mm(const f2 *src, float *out_g, long long 
         asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(addr) : "v"(idx), "v"(tap0));
         return reinterpret_cast<lds_f2 *>(static_cast<uintptr_t>(addr));
     };
-    double nt = 5.0 + 0.01 * lane, mu = 0.01 * lane, integ = 0.0;
+    double nt = (V == 10 ? 5.0 + (lane * 37) % 64 : 5.0) + 0.01 * lane, mu = 0.01 * lane, integ = 0.0;
     double psid = 0.3, psqd = -0.2, pdid = 1.0, pdqd = -1.0;
     lds_f2 *tp = taps_fl(floor(nt));
     f2 xm1 = tp[0], x0 = tp[1], x1 = tp[2], x2 = tp[3];
@@ -135,10 +141,10 @@ int main(int argc, char **argv) {
     f2 *src;
     float *out;
     long long *cyc;
-    hipMalloc(&src, 32 * kRow * sizeof(f2));
+    hipMalloc(&src, 32 * 262 * sizeof(f2));
     hipMalloc(&out, 64 * sizeof(float));
     hipMalloc(&cyc, 8);
-    f2 h[32 * kRow];
+    f2 h[32 * 262];
     unsigned s = 12345;
     for (auto &v : h) {
         s = s * 1664525u + 1013904223u;
@@ -157,5 +163,8 @@ int main(int argc, char **argv) {
     run<5>("TED without decision doubles", src, out, cyc, sps);
     run<6>("double symbol slot (ds_write_b128)", src, out, cyc, sps);
     run<7>("address off the chain + no store", src, out, cyc, sps);
+    run<8>("ring rows of 262 float2 (2-way conflicts)", src, out, cyc, sps);
+    run<9>("ring rows of 261 float2 (conflict-free)", src, out, cyc, sps);
+    run<10>("spread per-lane positions (rows of 260)", src, out, cyc, sps);
     return 0;
 }
