@@ -330,6 +330,7 @@ class BatchDemodulator:
         h = C.c_void_p()
         _check(lib().qpsk_demod_create(C.byref(p), self.S, C.byref(h)))
         self._h = h
+        self._bound = False   # set_stream(torch's stream) orders device calls on it
 
     def close(self):
         if getattr(self, "_h", None):
@@ -344,6 +345,19 @@ class BatchDemodulator:
 
     def set_stream(self, hip_stream_ptr: int | None):
         _check(lib().qpsk_demod_set_stream(self._h, C.c_void_p(hip_stream_ptr or 0)))
+        self._bound = bool(hip_stream_ptr)
+
+    def _after_torch(self, t):
+        """The handle's own stream (no set_stream) does not order against torch's:
+        wait for torch's queued work on the tensors (their zero-fills, copies)
+        before the library's kernels read or write them.  Round 6: with an
+        experimental faster matched filter, test_rows_past_4gib_bit_exact saw
+        its symbol rows' first entries zeroed after the loop kernel wrote them,
+        by the torch.zeros still queued on torch's stream
+        (profiles/r06_red_stream_race_gputest.log)."""
+        if not self._bound:
+            import torch
+            torch.cuda.current_stream(t.device).synchronize()
 
     def max_symbols(self, n: int) -> int:
         return int(lib().qpsk_demod_max_symbols(self._h, int(n)))
@@ -488,8 +502,10 @@ class BatchDemodulator:
     def process_device(self, iq_dev, n, bits_dev, n_bits_dev, mode=MODE_DEMODULATE,
                        syms_dev=None, n_syms_dev=None):
         """All arguments are torch CUDA tensors; stream-ordered on the handle's
-        stream (bind torch's stream with set_stream first)."""
+        stream (bind torch's stream with set_stream first; without it the call
+        first waits for torch's current stream)."""
         self._check_device_args(iq_dev, n, bits_dev, n_bits_dev, syms_dev, n_syms_dev)
+        self._after_torch(iq_dev)
         bstride = bits_dev.stride(0) * bits_dev.element_size() if bits_dev is not None else 0
         sstride = syms_dev.stride(0) if syms_dev is not None else 0
         _check(lib().qpsk_demod_process(
@@ -505,6 +521,7 @@ class BatchDemodulator:
         outputs are complete after pipeline_wait().  lengths: optional host
         int64 array of per-stream sample counts."""
         self._check_device_args(iq_dev, n, bits_dev, n_bits_dev, syms_dev, n_syms_dev)
+        self._after_torch(iq_dev)
         bstride = bits_dev.stride(0) * bits_dev.element_size() if bits_dev is not None else 0
         sstride = syms_dev.stride(0) if syms_dev is not None else 0
         if lengths is not None:
@@ -617,7 +634,10 @@ class DemodGroup:
     def process_device(self, iq_dev, n, bits_dev, n_bits_dev, mode=MODE_DEMODULATE, syms_dev=None,
                        n_syms_dev=None):
         """Device rows of the whole batch (every shard on one device): returns
-        with the outputs written."""
+        with the outputs written.  The shards run on their handles' own
+        streams, so the call first waits for torch's current stream."""
+        import torch
+        torch.cuda.current_stream(iq_dev.device).synchronize()
         bstride = bits_dev.stride(0) * bits_dev.element_size() if bits_dev is not None else 0
         sstride = syms_dev.stride(0) if syms_dev is not None else 0
         _check(lib().qpsk_demod_group_process(
