@@ -251,13 +251,30 @@ __global__ __launch_bounds__(NT) void fir_tile_kernel(FirArgs a, const float *hr
     {
         f2 *y = reinterpret_cast<f2 *>(a.y) + s * a.y_stride + a.y_offset;
         const int o0 = 64 * grp + r;
-        unsigned bad = 0;
+        // this thread's outputs from one base address (immediate store
+        // offsets); whole tiles, all but a row's last, skip the bounds tests
+        f2 *yt = y + tile0 + o0;
+        // any non-finite output: 0 * v is +-0 for finite v and NaN for NaN or
+        // +-Inf, so z = sum of 0 * acc stays +-0 unless one of them is not
+        // finite (an explicit fma: a test, not the reference's arithmetic).
+        // One class test instead of one per output (round 6)
+        f2 z = f2{0.0f, 0.0f};
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int64_t go = tile0 + o0 + W * q;
-            const bool nf = fir_nonfinite(acc[q].x) | fir_nonfinite(acc[q].y);
-            bad |= static_cast<unsigned>(nf) << q;
-            if (go < n) y[go] = acc[q];
+        for (int q = 0; q < Q; ++q) z = __builtin_elementwise_fma(acc[q], f2{0.0f, 0.0f}, z);
+        const bool any_bad = fir_nonfinite(z.x) | fir_nonfinite(z.y);
+        if (tile0 + TILE <= n) {
+#pragma unroll
+            for (int q = 0; q < Q; ++q) yt[W * q] = acc[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+                if (tile0 + o0 + W * q < n) yt[W * q] = acc[q];
+        }
+        unsigned bad = 0;
+        if (__builtin_expect(any_bad, 0)) {
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+                bad |= static_cast<unsigned>(fir_nonfinite(acc[q].x) | fir_nonfinite(acc[q].y)) << q;
         }
         if (ph_wg) {
             const unsigned long long p3 = __builtin_amdgcn_s_memtime();
